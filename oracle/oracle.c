@@ -1,0 +1,820 @@
+/* invsim ORACLE — test infrastructure only (see oracle.h).
+ *
+ * CPU restatement of the reference hot path.  Every function cites the
+ * reference file:line it restates.  Compile with -ffp-contract=off: the
+ * reference's arithmetic (numpy / CPython on x86-64 SSE2) never fuses a
+ * multiply-add, and neither may we.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+
+/* ======================================================================
+ * numpy SeedSequence (numpy/random/bit_generator.pyx, numpy 2.2.6):
+ * pool_size 4, hashmix/mix constants below, generate_state(4, uint64).
+ * Called by gymnasium.utils.seeding.np_random(seed) from Env.reset(seed=)
+ * (newsvendor.py:102, inventory_management.py:197, network_management.py:303).
+ * ==================================================================== */
+#define SS_INIT_A 0x43b0d7e5u
+#define SS_MULT_A 0x931e8875u
+#define SS_INIT_B 0x8b51f9ddu
+#define SS_MULT_B 0x58f38dedu
+#define SS_MIX_L 0xca01f9ddu
+#define SS_MIX_R 0x4973f715u
+
+static uint32_t ss_hashmix(uint32_t value, uint32_t *hc) {
+    value ^= *hc;
+    *hc *= SS_MULT_A;
+    value *= *hc;
+    value ^= value >> 16;
+    return value;
+}
+
+static uint32_t ss_mix(uint32_t x, uint32_t y) {
+    uint32_t r = SS_MIX_L * x - SS_MIX_R * y;
+    r ^= r >> 16;
+    return r;
+}
+
+static const u128 PCG_MULT = ((u128)0x2360ED051FC65DA4ULL << 64) | 0x4385DF649FCCF645ULL;
+
+void orc_seed_pcg64(const uint32_t *words, int nwords, uint64_t rng[4]) {
+    uint32_t pool[4];
+    uint32_t hc = SS_INIT_A;
+    for (int i = 0; i < 4; i++) pool[i] = ss_hashmix(i < nwords ? words[i] : 0u, &hc);
+    for (int s = 0; s < 4; s++)
+        for (int d = 0; d < 4; d++)
+            if (s != d) pool[d] = ss_mix(pool[d], ss_hashmix(pool[s], &hc));
+    for (int s = 4; s < nwords; s++)
+        for (int d = 0; d < 4; d++) pool[d] = ss_mix(pool[d], ss_hashmix(words[s], &hc));
+    uint32_t out[8];
+    uint32_t hb = SS_INIT_B;
+    for (int i = 0; i < 8; i++) {
+        uint32_t v = pool[i & 3];
+        v ^= hb;
+        hb *= SS_MULT_B;
+        v *= hb;
+        v ^= v >> 16;
+        out[i] = v;
+    }
+    uint64_t w64[4];
+    for (int k = 0; k < 4; k++) w64[k] = (uint64_t)out[2 * k] | ((uint64_t)out[2 * k + 1] << 32);
+    /* PCG64.__init__ -> pcg64_set_seed(seed = w64[0:2], inc = w64[2:4]):
+     * pcg_setseq_128_srandom_r: state=0; inc=(initseq<<1)|1; step; state+=initstate; step */
+    u128 initstate = ((u128)w64[0] << 64) | w64[1];
+    u128 initseq = ((u128)w64[2] << 64) | w64[3];
+    u128 inc = (initseq << 1) | 1u;
+    u128 st = 0;
+    st = st * PCG_MULT + inc;
+    st += initstate;
+    st = st * PCG_MULT + inc;
+    rng[0] = (uint64_t)(st >> 64);
+    rng[1] = (uint64_t)st;
+    rng[2] = (uint64_t)(inc >> 64);
+    rng[3] = (uint64_t)inc;
+}
+
+/* PCG64 XSL-RR 128/64 (numpy pcg64.h pcg64_next64) */
+uint64_t orc_next64(uint64_t rng[4]) {
+    u128 st = ((u128)rng[0] << 64) | rng[1];
+    u128 inc = ((u128)rng[2] << 64) | rng[3];
+    st = st * PCG_MULT + inc;
+    rng[0] = (uint64_t)(st >> 64);
+    rng[1] = (uint64_t)st;
+    uint64_t x = rng[0] ^ rng[1];
+    unsigned rot = (unsigned)(rng[0] >> 58);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+/* numpy next_double: (next64 >> 11) * 2^-53 */
+double orc_next_double(uint64_t rng[4]) {
+    return (double)(orc_next64(rng) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+/* numpy distributions.c random_loggam */
+double orc_loggam(double x) {
+    static const double a[10] = {8.333333333333333e-02, -2.777777777777778e-03,
+                                 7.936507936507937e-04, -5.952380952380952e-04,
+                                 8.417508417508418e-04, -1.917526917526918e-03,
+                                 6.410256410256410e-03, -2.955065359477124e-02,
+                                 1.796443723688307e-01, -1.39243221690590e+00};
+    int64_t n;
+    if (x == 1.0 || x == 2.0) return 0.0;
+    if (x < 7.0)
+        n = (int64_t)(7 - x);
+    else
+        n = 0;
+    double x0 = x + n;
+    double x2 = (1.0 / x0) * (1.0 / x0);
+    const double lg2pi = 1.8378770664093453e+00;
+    double gl0 = a[9];
+    for (int k = 8; k >= 0; k--) {
+        gl0 *= x2;
+        gl0 += a[k];
+    }
+    double gl = gl0 / x0 + 0.5 * lg2pi + (x0 - 0.5) * log(x0) - x0;
+    if (x < 7.0) {
+        for (int64_t k = 1; k <= n; k++) {
+            gl -= log(x0 - 1.0);
+            x0 -= 1.0;
+        }
+    }
+    return gl;
+}
+
+/* numpy distributions.c random_poisson_ptrs (lam >= 10) */
+static int64_t poisson_ptrs(uint64_t rng[4], double lam) {
+    double slam = sqrt(lam);
+    double loglam = log(lam);
+    double b = 0.931 + 2.53 * slam;
+    double a = -0.059 + 0.02483 * b;
+    double invalpha = 1.1239 + 1.1328 / (b - 3.4);
+    double vr = 0.9277 - 3.6224 / (b - 2);
+    for (;;) {
+        double U = orc_next_double(rng) - 0.5;
+        double V = orc_next_double(rng);
+        double us = 0.5 - fabs(U);
+        int64_t k = (int64_t)floor((2 * a / us + b) * U + lam + 0.43);
+        if ((us >= 0.07) && (V <= vr)) return k;
+        if ((k < 0) || ((us < 0.013) && (V > us))) continue;
+        if ((log(V) + log(invalpha) - log(a / (us * us) + b)) <=
+            (-lam + k * loglam - orc_loggam(k + 1)))
+            return k;
+    }
+}
+
+/* numpy distributions.c random_poisson_mult (0 < lam < 10) */
+static int64_t poisson_mult(uint64_t rng[4], double lam) {
+    double enlam = exp(-lam);
+    int64_t X = 0;
+    double prod = 1.0;
+    for (;;) {
+        double U = orc_next_double(rng);
+        prod *= U;
+        if (prod > enlam)
+            X += 1;
+        else
+            return X;
+    }
+}
+
+int64_t orc_poisson(uint64_t rng[4], double lam) {
+    if (lam >= 10) return poisson_ptrs(rng, lam);
+    if (lam == 0) return 0;
+    return poisson_mult(rng, lam);
+}
+
+void orc_poisson_fill(uint64_t rng[4], double lam, int64_t *out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) out[i] = orc_poisson(rng, lam);
+}
+
+/* numpy add.reduce for float32/float64 1-D contiguous input: identity 0 then
+ * pairwise_sum (loops_utils.h.src): n<8 sequential; n<=128 eight accumulators;
+ * else split at n/2 rounded down to a multiple of 8. */
+static float pw_f32(const float *a, int64_t n) {
+    if (n < 8) {
+        float res = 0.f;
+        for (int64_t i = 0; i < n; i++) res += a[i];
+        return res;
+    } else if (n <= 128) {
+        float r[8];
+        int64_t i;
+        for (int j = 0; j < 8; j++) r[j] = a[j];
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; j++) r[j] += a[i + j];
+        float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i];
+        return res;
+    } else {
+        int64_t n2 = n / 2;
+        n2 -= n2 % 8;
+        return pw_f32(a, n2) + pw_f32(a + n2, n - n2);
+    }
+}
+
+static double pw_f64(const double *a, int64_t n) {
+    if (n < 8) {
+        double res = 0.;
+        for (int64_t i = 0; i < n; i++) res += a[i];
+        return res;
+    } else if (n <= 128) {
+        double r[8];
+        int64_t i;
+        for (int j = 0; j < 8; j++) r[j] = a[j];
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; j++) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i];
+        return res;
+    } else {
+        int64_t n2 = n / 2;
+        n2 -= n2 % 8;
+        return pw_f64(a, n2) + pw_f64(a + n2, n - n2);
+    }
+}
+
+float orc_sum_f32(const float *a, int64_t n) { return 0.f + pw_f32(a, n); }
+double orc_sum_f64(const double *a, int64_t n) { return 0. + pw_f64(a, n); }
+
+/* ======================================================================
+ * NumPy-2 (NEP 50) scalar type lattice used by NewsvendorEnv.step.
+ * PY  = Python int/float ("weak": cast to the other operand's dtype)
+ * F32 = np.float32, F64 = np.float64.
+ * ==================================================================== */
+enum { K_PY = 0, K_F32 = 1, K_F64 = 2 };
+typedef struct {
+    double v;
+    int k;
+} tv;
+
+static tv tv_make(double v, int k) {
+    tv r;
+    r.v = v;
+    r.k = k;
+    return r;
+}
+
+static tv tv_bin(tv a, tv b, char op) {
+    tv r;
+    if (a.k == K_F64 || b.k == K_F64 || (a.k == K_PY && b.k == K_PY)) {
+        r.k = (a.k == K_F64 || b.k == K_F64) ? K_F64 : K_PY;
+        switch (op) {
+            case '+': r.v = a.v + b.v; break;
+            case '-': r.v = a.v - b.v; break;
+            default: r.v = a.v * b.v; break;
+        }
+    } else {
+        float fa = (float)a.v, fb = (float)b.v, fr;
+        switch (op) {
+            case '+': fr = fa + fb; break;
+            case '-': fr = fa - fb; break;
+            default: fr = fa * fb; break;
+        }
+        r.k = K_F32;
+        r.v = (double)fr;
+    }
+    return r;
+}
+
+/* ======================================================================
+ * NewsvendorEnv (newsvendor.py)
+ * ==================================================================== */
+typedef struct {
+    orc_nv_cfg c;
+    int64_t n;
+    uint64_t *rng;  /* [n][4] */
+    double *par;    /* [n][5] price, cost, h, k, mu (Python floats) */
+    float *state;   /* [n][L+5] self.state */
+    int32_t *step_count;
+} nv_t;
+
+void *orc_nv_create(const orc_nv_cfg *cfg, int64_t n) {
+    nv_t *h = (nv_t *)calloc(1, sizeof(nv_t));
+    h->c = *cfg;
+    if (h->c.lead_time < 0) h->c.lead_time = 0; /* newsvendor.py:65 max(0, lead_time) */
+    h->n = n;
+    h->rng = (uint64_t *)calloc((size_t)n * 4, sizeof(uint64_t));
+    h->par = (double *)calloc((size_t)n * 5, sizeof(double));
+    h->state = (float *)calloc((size_t)n * (h->c.lead_time + 5), sizeof(float));
+    h->step_count = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+    return h;
+}
+
+void orc_nv_destroy(void *p) {
+    nv_t *h = (nv_t *)p;
+    free(h->rng);
+    free(h->par);
+    free(h->state);
+    free(h->step_count);
+    free(h);
+}
+
+void orc_nv_seed(void *p, const uint32_t *words, const int32_t *nwords) {
+    nv_t *h = (nv_t *)p;
+    for (int64_t i = 0; i < h->n; i++) orc_seed_pcg64(words + 4 * i, nwords[i], h->rng + 4 * i);
+}
+
+/* newsvendor.py:100-123 */
+void orc_nv_reset(void *p, float *obs) {
+    nv_t *h = (nv_t *)p;
+    const int O = h->c.lead_time + 5;
+    for (int64_t i = 0; i < h->n; i++) {
+        uint64_t *rng = h->rng + 4 * i;
+        double *par = h->par + 5 * i;
+        double price = orc_next_double(rng) * h->c.p_max;
+        if (!(price > 1)) price = 1; /* max(1, x) */
+        double cost = orc_next_double(rng) * price;
+        if (!(cost > 1)) cost = 1;
+        double mn = (h->c.h_max < cost) ? h->c.h_max : cost; /* min(cost, h_max) */
+        double hh = orc_next_double(rng) * mn;
+        double kk = orc_next_double(rng) * h->c.k_max;
+        double mu = orc_next_double(rng) * h->c.mu_max;
+        par[0] = price;
+        par[1] = cost;
+        par[2] = hh;
+        par[3] = kk;
+        par[4] = mu;
+        float *st = h->state + (int64_t)O * i;
+        for (int j = 0; j < O; j++) st[j] = 0.f;
+        for (int j = 0; j < 5; j++) st[j] = (float)par[j];
+        h->step_count[i] = 0;
+        if (obs) memcpy(obs + (int64_t)O * i, st, sizeof(float) * O);
+    }
+}
+
+void orc_nv_get_params(void *p, double *params) {
+    nv_t *h = (nv_t *)p;
+    memcpy(params, h->par, sizeof(double) * 5 * h->n);
+}
+
+/* numpy clip for float64 (_NPY_CLIP: MIN(MAX(x, lo), hi), NaN propagates) */
+static double np_clip(double x, double lo, double hi) {
+    double y = isnan(x) ? x : (x > lo ? x : lo);
+    return isnan(y) ? y : (y < hi ? y : hi);
+}
+
+/* newsvendor.py:125-204 */
+void orc_nv_step(void *p, const float *action, float *obs, double *reward, uint8_t *truncated,
+                 int64_t *demand) {
+    nv_t *h = (nv_t *)p;
+    const int L = h->c.lead_time;
+    const int O = L + 5;
+    const tv ZERO = tv_make(0.0, K_PY);
+    for (int64_t i = 0; i < h->n; i++) {
+        uint64_t *rng = h->rng + 4 * i;
+        const double *par = h->par + 5 * i;
+        float *st = h->state + (int64_t)O * i;
+        h->step_count[i] += 1;                                                     /* :127 */
+        tv oq = tv_make(np_clip((double)action[i], 0, h->c.max_order_quantity), K_F64); /* :131-132 */
+        float S5 = orc_sum_f32(st + 5, L);                                         /* :135 */
+        tv inv = (L > 0) ? tv_make((double)st[5], K_F32) : oq;                     /* :136-141 */
+        tv cap = tv_bin(tv_make(h->c.max_inventory, K_PY), tv_make((double)S5, K_F32), '-');
+        tv m1 = (cap.v < oq.v) ? cap : oq;                                         /* min(oq, cap) */
+        tv q = (m1.v > 0) ? m1 : ZERO;                                             /* :143 max(0, .) */
+        int64_t d = orc_poisson(rng, par[4]);                                      /* :146 */
+        tv dv = tv_make((double)d, K_PY);
+        tv sales = (dv.v < inv.v) ? dv : inv;                                      /* :149 min(inv, d) */
+        tv price = tv_make(par[0], K_PY), cost = tv_make(par[1], K_PY);
+        tv hh = tv_make(par[2], K_PY), kk = tv_make(par[3], K_PY);
+        tv revenue = tv_bin(sales, price, '*');                                    /* :150 */
+        tv ex = tv_bin(inv, dv, '-');
+        tv excess = (ex.v > 0) ? ex : ZERO;                                        /* :152 */
+        tv sh = tv_bin(dv, inv, '-');
+        tv shortage = (sh.v > 0) ? sh : ZERO;                                      /* :153 */
+        tv purchase = tv_bin(q, cost, '*');                                        /* :162 */
+        tv holding = tv_bin(excess, hh, '*');                                      /* :166 */
+        tv penalty = tv_bin(shortage, kk, '*');                                    /* :167 */
+        tv r = tv_bin(tv_bin(tv_bin(revenue, purchase, '-'), holding, '-'), penalty, '-'); /* :170 */
+        if (L > 0) {                                                               /* :174-183 */
+            for (int j = 0; j < L - 1; j++) st[5 + j] = st[6 + j];
+            st[5 + L - 1] = (float)q.v;
+        }
+        reward[i] = r.v;
+        truncated[i] = (uint8_t)(h->step_count[i] >= h->c.step_limit);            /* :190 */
+        if (demand) demand[i] = d;
+        if (obs) memcpy(obs + (int64_t)O * i, st, sizeof(float) * O);
+    }
+}
+
+/* ======================================================================
+ * InvManagementMasterEnv (inventory_management.py)
+ * ==================================================================== */
+typedef struct {
+    int32_t m, m1, T, lt_max, O, backlog, dist;
+    double mu, alpha;
+    int64_t *I0, *c, *L, *user_D;
+    double up[64], uc[64], kc[64], hc[64]; /* f32 coefficients widened exactly */
+    int64_t n;
+    uint64_t *rng;
+    int64_t *I, *R, *B, *alog; /* per env histories */
+    int32_t *period;
+} im_t;
+
+void *orc_im_create(const orc_im_cfg *cfg, int64_t n) {
+    im_t *h = (im_t *)calloc(1, sizeof(im_t));
+    h->m = cfg->num_stages;
+    h->m1 = h->m - 1;
+    h->T = cfg->periods;
+    h->backlog = cfg->backlog;
+    h->dist = cfg->dist;
+    h->mu = cfg->mu;
+    h->alpha = cfg->alpha;
+    h->I0 = (int64_t *)malloc(sizeof(int64_t) * h->m1);
+    h->c = (int64_t *)malloc(sizeof(int64_t) * h->m1);
+    h->L = (int64_t *)malloc(sizeof(int64_t) * h->m1);
+    h->user_D = (int64_t *)calloc(h->T, sizeof(int64_t));
+    h->lt_max = 0;
+    for (int i = 0; i < h->m1; i++) {
+        h->I0[i] = cfg->I0[i];
+        h->c[i] = cfg->supply_capacity[i];
+        h->L[i] = cfg->lead_time[i];
+        if (h->L[i] > h->lt_max) h->lt_max = (int32_t)h->L[i]; /* :100 */
+    }
+    if (cfg->user_D)
+        for (int t = 0; t < h->T; t++) h->user_D[t] = cfg->user_D[t];
+    for (int j = 0; j < h->m; j++) {
+        h->up[j] = (double)cfg->unit_price[j];
+        h->uc[j] = (double)cfg->unit_cost[j];
+        h->kc[j] = (double)cfg->demand_cost[j];
+        h->hc[j] = (double)cfg->holding_cost[j];
+    }
+    h->O = h->m1 * (h->lt_max + 1); /* :119 */
+    h->n = n;
+    h->rng = (uint64_t *)calloc((size_t)n * 4, sizeof(uint64_t));
+    h->I = (int64_t *)calloc((size_t)n * (h->T + 1) * h->m1, sizeof(int64_t));
+    h->R = (int64_t *)calloc((size_t)n * (h->T + 1) * h->m1, sizeof(int64_t));
+    h->B = (int64_t *)calloc((size_t)n * (h->T + 1) * h->m, sizeof(int64_t));
+    h->alog = (int64_t *)calloc((size_t)n * (h->T + 1) * h->m1, sizeof(int64_t));
+    h->period = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+    return h;
+}
+
+void orc_im_destroy(void *p) {
+    im_t *h = (im_t *)p;
+    free(h->I0); free(h->c); free(h->L); free(h->user_D);
+    free(h->rng); free(h->I); free(h->R); free(h->B); free(h->alog); free(h->period);
+    free(h);
+}
+
+void orc_im_seed(void *p, const uint32_t *words, const int32_t *nwords) {
+    im_t *h = (im_t *)p;
+    for (int64_t i = 0; i < h->n; i++) orc_seed_pcg64(words + 4 * i, nwords[i], h->rng + 4 * i);
+}
+
+/* _get_obs :354-391 */
+static void im_obs(im_t *h, int64_t i, int64_t *obs) {
+    const int m1 = h->m1;
+    const int t = h->period[i];
+    const int64_t *I = h->I + (int64_t)i * (h->T + 1) * m1;
+    const int64_t *alog = h->alog + (int64_t)i * (h->T + 1) * m1;
+    int64_t *o = obs + (int64_t)h->O * i;
+    for (int j = 0; j < h->O; j++) o[j] = 0;
+    for (int j = 0; j < m1; j++) o[j] = I[(int64_t)t * m1 + j];
+    if (t > 0) {
+        int npast = t < h->lt_max ? t : h->lt_max;
+        for (int r = 0; r < npast; r++)
+            for (int j = 0; j < m1; j++) o[m1 + r * m1 + j] = alog[(int64_t)(t - npast + r) * m1 + j];
+    }
+}
+
+/* reset :186-222 (no RNG draws) */
+void orc_im_reset(void *p, int64_t *obs) {
+    im_t *h = (im_t *)p;
+    const int m1 = h->m1, m = h->m;
+    for (int64_t i = 0; i < h->n; i++) {
+        int64_t *I = h->I + (int64_t)i * (h->T + 1) * m1;
+        memset(I, 0, sizeof(int64_t) * (h->T + 1) * m1);
+        memset(h->R + (int64_t)i * (h->T + 1) * m1, 0, sizeof(int64_t) * (h->T + 1) * m1);
+        memset(h->B + (int64_t)i * (h->T + 1) * m, 0, sizeof(int64_t) * (h->T + 1) * m);
+        memset(h->alog + (int64_t)i * (h->T + 1) * m1, 0, sizeof(int64_t) * (h->T + 1) * m1);
+        for (int j = 0; j < m1; j++) I[j] = h->I0[j];
+        h->period[i] = 0;
+        if (obs) im_obs(h, i, obs);
+    }
+}
+
+/* numpy float64 -> int64 astype of an in-range value, and np.minimum(int64, f64) */
+static int64_t np_min_i64_f64(int64_t a, double b) {
+    double x = (double)a;
+    double r = (x <= b) ? x : b;
+    return (int64_t)r;
+}
+
+/* step :224-352 */
+void orc_im_step(void *p, const int64_t *action, int64_t *obs, double *reward, uint8_t *truncated,
+                 int64_t *demand, int64_t *sales, int64_t *unfulfilled, int64_t *ending_inventory,
+                 int64_t *backlog_next) {
+    im_t *h = (im_t *)p;
+    const int m1 = h->m1, m = h->m;
+    for (int64_t i = 0; i < h->n; i++) {
+        uint64_t *rng = h->rng + 4 * i;
+        const int t = h->period[i];
+        int64_t *I = h->I + (int64_t)i * (h->T + 1) * m1;
+        int64_t *R = h->R + (int64_t)i * (h->T + 1) * m1;
+        int64_t *B = h->B + (int64_t)i * (h->T + 1) * m;
+        int64_t *alog = h->alog + (int64_t)i * (h->T + 1) * m1;
+        int64_t req[64], ordreq[64], Rf[64], Icur[64], S[65], U[65];
+        for (int j = 0; j < m1; j++) {
+            int64_t a = action[(int64_t)i * m1 + j];
+            req[j] = a > 0 ? a : 0;                                   /* :250 */
+            ordreq[j] = req[j];
+            if (t >= 1) ordreq[j] = (int64_t)((uint64_t)ordreq[j] + (uint64_t)B[(int64_t)t * m + 1 + j]); /* :254-255 */
+        }
+        for (int j = 0; j < m1; j++) {
+            int64_t r = ordreq[j] < h->c[j] ? ordreq[j] : h->c[j];    /* :263 */
+            double sup = (j + 1 < m1) ? (double)I[(int64_t)t * m1 + j + 1] : INFINITY; /* :260 */
+            Rf[j] = np_min_i64_f64(r, sup);                           /* :265 */
+            R[(int64_t)t * m1 + j] = Rf[j];                           /* :267 */
+            alog[(int64_t)t * m1 + j] = req[j];                       /* :268 */
+        }
+        for (int j = 0; j < m1; j++) {                                /* :271-277 */
+            Icur[j] = I[(int64_t)t * m1 + j];
+            if (t - h->L[j] >= 0) Icur[j] += R[(int64_t)(t - h->L[j]) * m1 + j];
+        }
+        int64_t d;
+        if (h->dist == 5)
+            d = t < h->T ? h->user_D[t] : 0;                          /* :182 */
+        else
+            d = orc_poisson(rng, h->mu);                              /* :172 */
+        if (d < 0) d = 0;                                             /* :280 */
+        int64_t dfill = d;
+        if (t >= 1) dfill += B[(int64_t)t * m + 0];                   /* :285-286 */
+        int64_t s0 = Icur[0] < dfill ? Icur[0] : dfill;               /* :288 */
+        Icur[0] -= s0;
+        S[0] = s0;
+        for (int j = 0; j < m1; j++) S[j + 1] = Rf[j];                /* :295 */
+        for (int j = 1; j < m1; j++) Icur[j] -= Rf[j];                /* :300 (reference quirk) */
+        U[0] = dfill - s0;                                            /* :303 */
+        for (int j = 0; j < m1; j++) U[j + 1] = ordreq[j] - Rf[j];    /* :304 */
+        for (int j = 0; j < m; j++) B[(int64_t)(t + 1) * m + j] = h->backlog ? U[j] : 0; /* :307-312 */
+        double terms[65];
+        for (int j = 0; j < m; j++) {                                 /* :315-321 */
+            double Sj = (double)S[j];
+            int64_t inv = (j < m1) ? Icur[j] : 0;
+            double hold = h->hc[j] * (double)(inv > 0 ? inv : 0);
+            terms[j] = ((h->up[j] * Sj - h->uc[j] * Sj) - hold) - h->kc[j] * (double)U[j];
+        }
+        double profit = orc_sum_f64(terms, m);
+        double disc = pow(h->alpha, (double)t) * profit;             /* :322 */
+        for (int j = 0; j < m1; j++) I[(int64_t)(t + 1) * m1 + j] = Icur[j]; /* :326 */
+        h->period[i] = t + 1;
+        reward[i] = disc;
+        truncated[i] = (uint8_t)(h->period[i] >= h->T);               /* :350 */
+        if (obs) im_obs(h, i, obs);
+        if (demand) demand[i] = d;
+        if (sales) for (int j = 0; j < m; j++) sales[(int64_t)i * m + j] = S[j];
+        if (unfulfilled) for (int j = 0; j < m; j++) unfulfilled[(int64_t)i * m + j] = U[j];
+        if (ending_inventory) for (int j = 0; j < m1; j++) ending_inventory[(int64_t)i * m1 + j] = Icur[j];
+        if (backlog_next) for (int j = 0; j < m; j++) backlog_next[(int64_t)i * m + j] = B[(int64_t)(t + 1) * m + j];
+    }
+}
+
+/* ======================================================================
+ * NetInvMgmtMasterEnv (network_management.py)
+ * ==================================================================== */
+typedef struct {
+    orc_net_cfg c; /* pointers copied below */
+    int32_t J, E, RL, T, O, backlog;
+    double alpha;
+    double *I0, *h, *C, *o, *v;
+    int32_t *is_factory, *is_retail, *sup, *pur, *L, *sup_is_factory, *rl_node, *rl_user;
+    double *lp, *lg, *rl_p, *rl_b, *rl_lam, *user_D;
+    int32_t *succ_n, *succ_kind, *succ_idx, *pred_n, *pred_idx;
+    int64_t n;
+    uint64_t *rng;
+    double *X, *Y, *R, *S, *U, *D;
+    int32_t *period;
+} net_t;
+
+#define DUP(dst, src, cnt, ty)                                  \
+    do {                                                        \
+        dst = (ty *)calloc((size_t)((cnt) > 0 ? (cnt) : 1), sizeof(ty)); \
+        if (src) memcpy(dst, src, sizeof(ty) * (size_t)(cnt));  \
+    } while (0)
+
+void *orc_net_create(const orc_net_cfg *cfg, int64_t n) {
+    net_t *h = (net_t *)calloc(1, sizeof(net_t));
+    h->J = cfg->J;
+    h->E = cfg->E;
+    h->RL = cfg->RL;
+    h->T = cfg->num_periods;
+    h->backlog = cfg->backlog;
+    h->alpha = cfg->alpha;
+    DUP(h->I0, cfg->I0, h->J, double);
+    DUP(h->h, cfg->h, h->J, double);
+    DUP(h->C, cfg->C, h->J, double);
+    DUP(h->o, cfg->o, h->J, double);
+    DUP(h->v, cfg->v, h->J, double);
+    DUP(h->is_factory, cfg->is_factory, h->J, int32_t);
+    DUP(h->is_retail, cfg->is_retail, h->J, int32_t);
+    DUP(h->sup, cfg->sup, h->E, int32_t);
+    DUP(h->pur, cfg->pur, h->E, int32_t);
+    DUP(h->L, cfg->L, h->E, int32_t);
+    DUP(h->sup_is_factory, cfg->sup_is_factory, h->E, int32_t);
+    DUP(h->lp, cfg->lp, h->E, double);
+    DUP(h->lg, cfg->lg, h->E, double);
+    DUP(h->rl_node, cfg->rl_node, h->RL, int32_t);
+    DUP(h->rl_p, cfg->rl_p, h->RL, double);
+    DUP(h->rl_b, cfg->rl_b, h->RL, double);
+    DUP(h->rl_lam, cfg->rl_lam, h->RL, double);
+    DUP(h->rl_user, cfg->rl_user, h->RL, int32_t);
+    DUP(h->user_D, cfg->user_D, h->RL * h->T, double);
+    DUP(h->succ_n, cfg->succ_n, h->J, int32_t);
+    DUP(h->succ_kind, cfg->succ_kind, h->J * ORC_NET_MAXADJ, int32_t);
+    DUP(h->succ_idx, cfg->succ_idx, h->J * ORC_NET_MAXADJ, int32_t);
+    DUP(h->pred_n, cfg->pred_n, h->J, int32_t);
+    DUP(h->pred_idx, cfg->pred_idx, h->J * ORC_NET_MAXADJ, int32_t);
+    int sumL = 0;
+    for (int e = 0; e < h->E; e++) sumL += h->L[e];
+    h->O = h->RL + h->J + sumL; /* :188-190 */
+    h->n = n;
+    h->rng = (uint64_t *)calloc((size_t)n * 4, sizeof(uint64_t));
+    h->X = (double *)calloc((size_t)n * (h->T + 2) * h->J, sizeof(double));
+    h->Y = (double *)calloc((size_t)n * (h->T + 2) * (h->E ? h->E : 1), sizeof(double));
+    h->R = (double *)calloc((size_t)n * (h->T + 2) * (h->E ? h->E : 1), sizeof(double));
+    h->S = (double *)calloc((size_t)n * (h->T + 2) * (h->E + h->RL + 1), sizeof(double));
+    h->U = (double *)calloc((size_t)n * (h->T + 2) * (h->RL ? h->RL : 1), sizeof(double));
+    h->D = (double *)calloc((size_t)n * (h->T + 2) * (h->RL ? h->RL : 1), sizeof(double));
+    h->period = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+    return h;
+}
+
+void orc_net_destroy(void *p) {
+    net_t *h = (net_t *)p;
+    free(h->I0); free(h->h); free(h->C); free(h->o); free(h->v);
+    free(h->is_factory); free(h->is_retail); free(h->sup); free(h->pur); free(h->L);
+    free(h->sup_is_factory); free(h->lp); free(h->lg); free(h->rl_node); free(h->rl_p);
+    free(h->rl_b); free(h->rl_lam); free(h->rl_user); free(h->user_D); free(h->succ_n);
+    free(h->succ_kind); free(h->succ_idx); free(h->pred_n); free(h->pred_idx);
+    free(h->rng); free(h->X); free(h->Y); free(h->R); free(h->S); free(h->U); free(h->D);
+    free(h->period);
+    free(h);
+}
+
+int32_t orc_net_obs_dim(void *p) { return ((net_t *)p)->O; }
+
+void orc_net_seed(void *p, const uint32_t *words, const int32_t *nwords) {
+    net_t *h = (net_t *)p;
+    for (int64_t i = 0; i < h->n; i++) orc_seed_pcg64(words + 4 * i, nwords[i], h->rng + 4 * i);
+}
+
+#define NX(h, i) ((h)->X + (int64_t)(i) * ((h)->T + 2) * (h)->J)
+#define NY(h, i) ((h)->Y + (int64_t)(i) * ((h)->T + 2) * ((h)->E ? (h)->E : 1))
+#define NR(h, i) ((h)->R + (int64_t)(i) * ((h)->T + 2) * ((h)->E ? (h)->E : 1))
+#define NS(h, i) ((h)->S + (int64_t)(i) * ((h)->T + 2) * ((h)->E + (h)->RL + 1))
+#define NU(h, i) ((h)->U + (int64_t)(i) * ((h)->T + 2) * ((h)->RL ? (h)->RL : 1))
+#define ND(h, i) ((h)->D + (int64_t)(i) * ((h)->T + 2) * ((h)->RL ? (h)->RL : 1))
+
+/* _get_obs :334-413 */
+static void net_obs(net_t *h, int64_t i, float *obs) {
+    const int t = h->period[i];
+    const int E = h->E ? h->E : 1, RLs = h->RL ? h->RL : 1;
+    float *o = obs + (int64_t)h->O * i;
+    int k = 0;
+    for (int r = 0; r < h->RL; r++) o[k++] = (float)NU(h, i)[(int64_t)t * RLs + r];
+    for (int j = 0; j < h->J; j++) o[k++] = (float)NX(h, i)[(int64_t)t * h->J + j];
+    for (int e = 0; e < h->E; e++) {
+        int L = h->L[e];
+        if (L == 0) continue;
+        int start = t - L > 0 ? t - L : 0;
+        if (start > h->T - 1) start = h->T - 1;
+        int end = t < h->T ? t : h->T;
+        float *pad = o + k;
+        for (int q = 0; q < L; q++) pad[q] = 0.f;
+        int cnt = end - start;
+        if (cnt > 0)
+            for (int q = 0; q < cnt; q++) pad[L - cnt + q] = (float)NR(h, i)[(int64_t)(start + q) * E + e];
+        k += L;
+    }
+}
+
+/* reset :301-332 (no RNG draws) */
+void orc_net_reset(void *p, float *obs) {
+    net_t *h = (net_t *)p;
+    const int E = h->E ? h->E : 1, RLs = h->RL ? h->RL : 1;
+    for (int64_t i = 0; i < h->n; i++) {
+        memset(NX(h, i), 0, sizeof(double) * (h->T + 2) * h->J);
+        memset(NY(h, i), 0, sizeof(double) * (h->T + 2) * E);
+        memset(NR(h, i), 0, sizeof(double) * (h->T + 2) * E);
+        memset(NS(h, i), 0, sizeof(double) * (h->T + 2) * (h->E + h->RL + 1));
+        memset(NU(h, i), 0, sizeof(double) * (h->T + 2) * RLs);
+        memset(ND(h, i), 0, sizeof(double) * (h->T + 2) * RLs);
+        for (int j = 0; j < h->J; j++) NX(h, i)[j] = h->I0[j];
+        h->period[i] = 0;
+        if (obs) net_obs(h, i, obs);
+    }
+}
+
+static double py_max0(double x) { return (x > 0) ? x : 0.0; } /* max(0, x) */
+
+/* step :436-635 */
+void orc_net_step(void *p, const float *action, float *obs, double *reward, uint8_t *truncated,
+                  double *Xo, double *Uo, double *Do, double *Ro, double *Yo, double *Po) {
+    net_t *h = (net_t *)p;
+    const int J = h->J, EE = h->E, RL = h->RL;
+    const int E = EE ? EE : 1, RLs = RL ? RL : 1, SL = h->E + h->RL + 1;
+    double cons[64], arr[64], xb[64], prof[64];
+    for (int64_t i = 0; i < h->n; i++) {
+        uint64_t *rng = h->rng + 4 * i;
+        const int t = h->period[i];
+        double *X = NX(h, i), *Y = NY(h, i), *R = NR(h, i), *S = NS(h, i), *U = NU(h, i), *D = ND(h, i);
+        for (int j = 0; j < J; j++) cons[j] = 0.0, arr[j] = 0.0;
+        /* 0) orders, sorted reorder links :448-490 */
+        for (int e = 0; e < EE; e++) {
+            double raw = (double)action[(int64_t)i * EE + e];
+            double rq = nearbyint(raw);                   /* round() half-to-even */
+            double request = (rq > 0) ? rq : 0.0;         /* max(0, .) */
+            double f;
+            int s = h->sup[e];
+            if (s < 0) {
+                f = request;                              /* raw material: unlimited */
+            } else {
+                double avail = X[(int64_t)t * J + s] - cons[s];
+                double oav = py_max0(avail);
+                double order_available = oav;
+                if (h->sup_is_factory[e]) {
+                    double mpi = h->v[s] * oav;
+                    double mp = (mpi < h->C[s]) ? mpi : h->C[s]; /* min(C, mpi) */
+                    order_available = (mp < order_available) ? mp : order_available;
+                }
+                f = (order_available < request) ? order_available : request; /* min(request, avail) */
+                cons[s] += f / h->v[s];                  /* v = node.get('v', 1.0) */
+            }
+            R[(int64_t)t * E + e] = f;
+            S[(int64_t)t * SL + e] = f;
+        }
+        /* 1) pipeline :494-511 */
+        for (int e = 0; e < EE; e++) {
+            int L = h->L[e];
+            double arrv = 0.0;
+            if (t - L >= 0 && t - L < h->T) arrv = R[(int64_t)(t - L) * E + e];
+            Y[(int64_t)(t + 1) * E + e] = Y[(int64_t)t * E + e] - arrv + R[(int64_t)t * E + e];
+        }
+        /* arrivals :516-523 */
+        for (int j = 0; j < J; j++) {
+            for (int q = 0; q < h->pred_n[j]; q++) {
+                int e = h->pred_idx[j * ORC_NET_MAXADJ + q];
+                int L = h->L[e];
+                if (t - L >= 0 && t - L < h->T) arr[j] += R[(int64_t)(t - L) * E + e];
+            }
+        }
+        for (int j = 0; j < J; j++) X[(int64_t)(t + 1) * J + j] = X[(int64_t)t * J + j] + arr[j] - cons[j]; /* :528 */
+        /* 2&3) market :536-566 */
+        for (int j = 0; j < J; j++) xb[j] = X[(int64_t)(t + 1) * J + j];
+        for (int r = 0; r < RL; r++) {
+            double dd;
+            if (h->rl_user[r]) {
+                int idx = t < h->T - 1 ? t : h->T - 1;
+                dd = h->user_D[(int64_t)r * h->T + idx];
+                dd = nearbyint(dd);                        /* max(0, int(round(x))) */
+                if (!(dd > 0)) dd = 0.0;
+            } else {
+                int64_t pd = orc_poisson(rng, h->rl_lam[r]);
+                dd = (double)(pd > 0 ? pd : 0);
+            }
+            D[(int64_t)t * RLs + r] = dd;
+            double fill = dd + U[(int64_t)t * RLs + r];
+            int node = h->rl_node[r];
+            double inv = py_max0(xb[node]);
+            double sale = (inv < fill) ? inv : fill;       /* min(fill, inv) */
+            S[(int64_t)t * SL + EE + r] = sale;
+            xb[node] -= sale;
+            double unf = fill - sale;
+            U[(int64_t)(t + 1) * RLs + r] = h->backlog ? unf : 0.0;
+        }
+        for (int j = 0; j < J; j++) X[(int64_t)(t + 1) * J + j] = xb[j]; /* :571 */
+        /* 5) profit :578-613 */
+        double total = 0.0;
+        for (int j = 0; j < J; j++) {
+            double SR = 0.0, PC = 0.0, HCp = 0.0, OC = 0.0, UP = 0.0, sold = 0.0;
+            for (int q = 0; q < h->succ_n[j]; q++) {
+                int kind = h->succ_kind[j * ORC_NET_MAXADJ + q], idx = h->succ_idx[j * ORC_NET_MAXADJ + q];
+                double pr = kind == 0 ? h->lp[idx] : h->rl_p[idx];
+                double sv = kind == 0 ? S[(int64_t)t * SL + idx] : S[(int64_t)t * SL + EE + idx];
+                SR += pr * sv;
+            }
+            for (int q = 0; q < h->pred_n[j]; q++) {
+                int e = h->pred_idx[j * ORC_NET_MAXADJ + q];
+                PC += h->lp[e] * R[(int64_t)t * E + e];
+            }
+            double HC_on = h->h[j] * py_max0(X[(int64_t)(t + 1) * J + j]);
+            for (int q = 0; q < h->pred_n[j]; q++) {
+                int e = h->pred_idx[j * ORC_NET_MAXADJ + q];
+                HCp += h->lg[e] * py_max0(Y[(int64_t)(t + 1) * E + e]);
+            }
+            double HC = HC_on + HCp;
+            if (h->is_factory[j]) {
+                for (int q = 0; q < h->succ_n[j]; q++) {
+                    int kind = h->succ_kind[j * ORC_NET_MAXADJ + q], idx = h->succ_idx[j * ORC_NET_MAXADJ + q];
+                    sold += kind == 0 ? S[(int64_t)t * SL + idx] : S[(int64_t)t * SL + EE + idx];
+                }
+                OC = (h->v[j] > 0) ? h->o[j] * (sold / h->v[j]) : 0.0;
+            }
+            if (h->is_retail[j]) {
+                for (int q = 0; q < h->succ_n[j]; q++) {
+                    if (h->succ_kind[j * ORC_NET_MAXADJ + q] != 1) continue;
+                    int r = h->succ_idx[j * ORC_NET_MAXADJ + q];
+                    UP += h->rl_b[r] * U[(int64_t)(t + 1) * RLs + r];
+                }
+            }
+            double np_ = SR - PC - OC - HC - UP;
+            prof[j] = np_;
+            total += np_;
+        }
+        double disc = pow(h->alpha, (double)t) * total; /* :619 */
+        h->period[i] = t + 1;
+        reward[i] = disc;
+        truncated[i] = (uint8_t)(h->period[i] >= h->T);
+        if (obs) net_obs(h, i, obs);
+        if (Xo) for (int j = 0; j < J; j++) Xo[(int64_t)i * J + j] = X[(int64_t)(t + 1) * J + j];
+        if (Uo) for (int r = 0; r < RL; r++) Uo[(int64_t)i * RL + r] = U[(int64_t)(t + 1) * RLs + r];
+        if (Do) for (int r = 0; r < RL; r++) Do[(int64_t)i * RL + r] = D[(int64_t)t * RLs + r];
+        if (Ro) for (int e = 0; e < EE; e++) Ro[(int64_t)i * EE + e] = R[(int64_t)t * E + e];
+        if (Yo) for (int e = 0; e < EE; e++) Yo[(int64_t)i * EE + e] = Y[(int64_t)(t + 1) * E + e];
+        if (Po) for (int j = 0; j < J; j++) Po[(int64_t)i * J + j] = prof[j];
+    }
+}
