@@ -1,0 +1,188 @@
+/* invsim — MI355X-native vectorised inventory-simulation engine: C ABI.
+ *
+ * This is the drop-in boundary for the reference's hot path, the Gymnasium
+ * `Env.reset()` / `Env.step()` pair of the five environment classes of
+ * jacklu2016/or-gym-inventory.  One handle = one batch of N independent env
+ * instances of one class, resident in HBM (SoA state), bound to one GPU.
+ *
+ *   reference interface                                  replaced by
+ *   ---------------------------------------------------  ----------------------------------
+ *   NewsvendorEnv.__init__            newsvendor.py:52-97   invsim_create_newsvendor
+ *   InvManagementMasterEnv.__init__   inventory_management.py:48-141
+ *     (+ Backlog/LostSales subclasses :429-451)            invsim_create_invmgmt
+ *   NetInvMgmtMasterEnv.__init__      network_management.py:55-106,146-195
+ *     (+ Backlog/LostSales subclasses :747-770)            invsim_create_netinvmgmt
+ *   gym.Env.reset(seed=s) -> seeding.np_random(s)
+ *     (newsvendor.py:102, inventory_management.py:197,
+ *      network_management.py:303)                          invsim_seed_range / invsim_seed_words
+ *   Env.reset()  newsvendor.py:100-123,
+ *                inventory_management.py:186-222,
+ *                network_management.py:301-332              invsim_reset
+ *   Env.step()   newsvendor.py:125-204,
+ *                inventory_management.py:224-352,
+ *                network_management.py:436-635              invsim_step
+ *   K x Env.step() with pre-computed actions                invsim_rollout
+ *   (no reference equivalent: env state is never
+ *    checkpointed there)                                   invsim_state_* / invsim_get_state / invsim_set_state
+ *
+ * Conventions
+ *  - Every buffer argument of reset/step/rollout/seed/state calls is a DEVICE
+ *    pointer on the handle's GPU, owned by the caller.  Spec structs passed to
+ *    invsim_create_* are HOST memory and are copied.
+ *  - `stream` is a hipStream_t (NULL = default stream).  Calls are
+ *    asynchronous on that stream; the library never synchronises.
+ *  - Dtypes follow the reference spaces: Newsvendor obs/action f32;
+ *    InvMgmt obs/action int64; NetInvMgmt obs/action f32.  Rewards f64.
+ *    terminated/truncated are uint8 (0/1).
+ *  - Return 0 on success, a negative errno-style code on failure;
+ *    invsim_last_error(h) (or invsim_last_error(NULL) after a failed create)
+ *    gives the message.  No exceptions cross the ABI.
+ *  - A handle is not thread-safe.  One handle per GPU per process.
+ */
+#ifndef INVSIM_H
+#define INVSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define INVSIM_ABI_VERSION 1
+
+#define INVSIM_OK 0
+#define INVSIM_EINVAL (-22)
+#define INVSIM_ENOMEM (-12)
+#define INVSIM_EDEVICE (-5)
+#define INVSIM_ERANGE (-34)
+
+/* Env families */
+#define INVSIM_NEWSVENDOR 1
+#define INVSIM_INVMGMT 2
+#define INVSIM_NETINVMGMT 3
+
+/* Vector autoreset modes (gymnasium.vector.AutoresetMode) */
+#define INVSIM_AUTORESET_NEXT_STEP 0 /* gymnasium >= 1.0 default: reset on the step after done   */
+#define INVSIM_AUTORESET_SAME_STEP 1 /* SB3 VecEnv: reset in the done step, final obs separately */
+#define INVSIM_AUTORESET_DISABLED 2  /* caller resets explicitly                                   */
+
+typedef struct invsim_handle invsim_handle;
+
+/* newsvendor.py:52-61 constructor arguments */
+typedef struct {
+    int32_t lead_time;         /* <0 is clamped to 0 (:65); at most 128 */
+    int32_t step_limit;
+    double max_inventory;
+    double max_order_quantity;
+    double p_max, h_max, k_max, mu_max;
+    double gamma;              /* accepted, unused by the dynamics (as in the reference) */
+} invsim_newsvendor_spec;
+
+/* inventory_management.py:48-101 after parameter processing.  Coefficient
+ * arrays are the reference's float32 arrays (:89-92). */
+typedef struct {
+    int32_t num_stages;              /* m = len(I0) + 1, 2..9 */
+    int32_t periods;
+    int32_t backlog;                 /* 1 = InvManagementBacklogEnv, 0 = LostSales */
+    int32_t dist;                    /* 1 = Poisson(mu); 5 = user_D */
+    double mu;                       /* dist_param['mu'] */
+    double alpha;                    /* discount; reward *= alpha**t */
+    const int64_t *I0;               /* [m-1] */
+    const float *unit_price;         /* [m] = append(p, r[:-1]) */
+    const float *unit_cost;          /* [m] = r */
+    const float *demand_cost;        /* [m] = k */
+    const float *holding_cost;       /* [m] = append(h, 0) */
+    const int64_t *supply_capacity;  /* [m-1] = c */
+    const int64_t *lead_time;        /* [m-1] = L, each 0..255 */
+    const int64_t *user_D;           /* [periods], dist == 5 only (else NULL) */
+} invsim_invmgmt_spec;
+
+/* network_management.py:146-195 classification, compiled to index tables by
+ * the host (main nodes sorted; reorder links sorted; retail links in graph
+ * edge order; adjacency lists in graph adjacency order). */
+typedef struct {
+    int32_t n_main;      /* J */
+    int32_t n_reorder;   /* E  (= action dim) */
+    int32_t n_retail;    /* RL */
+    int32_t num_periods;
+    int32_t backlog;     /* EFFECTIVE flag (the reference LostSales class runs backlog=True) */
+    double alpha;
+    /* main nodes [J] */
+    const double *I0, *h, *C, *o, *v;
+    const int32_t *is_factory, *is_retail;
+    /* reorder links [E] */
+    const int32_t *sup;             /* supplier main-node index, -1 = raw material */
+    const int32_t *pur;             /* purchaser main-node index */
+    const int32_t *sup_is_factory;
+    const int32_t *L;               /* lead time, 0..255 */
+    const double *lp, *lg;          /* price p, pipeline holding g */
+    /* retail links [RL] */
+    const int32_t *rl_node;         /* retailer main-node index */
+    const double *rl_p, *rl_b, *rl_lam;
+    const int32_t *rl_user;         /* 1: demand = user_D row (network_management.py:250-255) */
+    const double *user_D;           /* [RL][num_periods] or NULL */
+    /* CSR adjacency.  succ: successors of each main node (kind 0 = reorder link idx,
+     * kind 1 = retail link idx); pred: reorder links into each main node. */
+    const int32_t *succ_ptr;        /* [J+1] */
+    const int32_t *succ_kind;       /* [succ_ptr[J]] */
+    const int32_t *succ_idx;        /* [succ_ptr[J]] */
+    const int32_t *pred_ptr;        /* [J+1] */
+    const int32_t *pred_idx;        /* [pred_ptr[J]] */
+} invsim_netinvmgmt_spec;
+
+int invsim_abi_version(void);
+const char *invsim_last_error(const invsim_handle *h);
+
+int invsim_create_newsvendor(const invsim_newsvendor_spec *spec, int64_t n_envs, int32_t device,
+                             int32_t autoreset_mode, invsim_handle **out);
+int invsim_create_invmgmt(const invsim_invmgmt_spec *spec, int64_t n_envs, int32_t device,
+                          int32_t autoreset_mode, invsim_handle **out);
+int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *spec, int64_t n_envs, int32_t device,
+                             int32_t autoreset_mode, invsim_handle **out);
+void invsim_destroy(invsim_handle *h);
+
+/* obs_dim, action_dim, number of demand draws per step (info_demand width), env family */
+int invsim_dims(const invsim_handle *h, int32_t *obs_dim, int32_t *action_dim, int32_t *demand_dim,
+                int32_t *family);
+int invsim_set_autoreset(invsim_handle *h, int32_t mode);
+
+/* Seeding = gymnasium seeding.np_random(seed): numpy SeedSequence(seed) -> PCG64.
+ * seed_range: env i (mask[i] != 0, or all when mask == NULL) gets the 128-bit
+ * integer seed  base + first_index + i  (gymnasium SyncVectorEnv: seed + i).
+ * seed_words: env i gets the little-endian uint32 entropy words[i][0..nwords[i]). */
+int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int64_t first_index,
+                      const uint8_t *mask, void *stream);
+int invsim_seed_words(invsim_handle *h, const uint32_t *words /*[N][4]*/,
+                      const int32_t *nwords /*[N]*/, const uint8_t *mask, void *stream);
+
+/* Env.reset() on every env (mask NULL) or on mask[i] != 0; writes obs rows of
+ * the reset envs (obs may be NULL).  RNG streams continue (reset without seed). */
+int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream);
+
+/* One Env.step() on all N envs.  actions [N][A]; obs [N][O]; reward [N];
+ * terminated/truncated [N]; final_obs [N][O] (SAME_STEP mode only, may be NULL). */
+int invsim_step(invsim_handle *h, const void *actions, void *obs, double *reward,
+                uint8_t *terminated, uint8_t *truncated, void *final_obs, void *stream);
+
+/* K consecutive steps in one launch (state held in registers between steps):
+ * identical results to K invsim_step calls.  actions [K][N][A]; obs [K][N][O];
+ * reward/terminated/truncated [K][N]. */
+int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, double *reward,
+                   uint8_t *terminated, uint8_t *truncated, void *stream);
+
+/* Optional per-step demand record (info['demand'] / D): int64 [N][demand_dim],
+ * written by every subsequent step/rollout(last step) when non-NULL. */
+int invsim_set_info_demand(invsim_handle *h, int64_t *demand);
+
+/* Checkpoint / debug: the full device state as one opaque blob of state_bytes,
+ * plus a field directory (name, byte offset, element size, rows) for tests. */
+int invsim_state_bytes(const invsim_handle *h, int64_t *bytes);
+int invsim_state_field(const invsim_handle *h, int32_t idx, char name[32], int64_t *offset,
+                       int32_t *elem_bytes, int32_t *rows, int64_t *row_stride);
+int invsim_get_state(invsim_handle *h, void *dst, void *stream);
+int invsim_set_state(invsim_handle *h, const void *src, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INVSIM_H */

@@ -1,0 +1,630 @@
+// C ABI of libinvsim (include/invsim.h): handle lifetime, HBM state arena,
+// spec validation (the reference's assert checks), and kernel launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/invsim.h"
+#include "kernels.hpp"
+
+using namespace invsim;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct Field {
+    std::string name;
+    int64_t offset;   // bytes from arena start
+    int32_t elem;     // element bytes
+    int32_t rows;
+};
+
+}  // namespace
+
+struct invsim_handle {
+    int32_t family = 0;
+    int32_t device = 0;
+    int64_t N = 0, Npad = 0;
+    int32_t obs_dim = 0, act_dim = 0, demand_dim = 1;
+    char *arena = nullptr;      // state (get/set_state blob)
+    int64_t arena_bytes = 0;
+    char *tables = nullptr;     // read-only tables (not part of the state blob)
+    std::vector<Field> fields;
+    Common cm{};
+    NvParams nv{};
+    ImParams im{};
+    NetParams net{};
+    int32_t im_m1 = 0;
+    bool im_backlog = false;
+    std::string err;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int fail(invsim_handle *h, int code, const std::string &msg) {
+    if (h) h->err = msg;
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(invsim_handle *h, hipError_t e, const char *what) {
+    return fail(h, INVSIM_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Lay out named SoA fields (rows x Npad elements each, 256-byte aligned).
+struct Layout {
+    std::vector<Field> f;
+    int64_t bytes = 0;
+    int64_t add(const char *name, int32_t elem, int32_t rows, int64_t npad) {
+        bytes = (bytes + 255) / 256 * 256;
+        Field x{name, bytes, elem, rows};
+        f.push_back(x);
+        bytes += (int64_t)elem * rows * npad;
+        return x.offset;
+    }
+};
+
+template <typename T>
+T *at(invsim_handle *h, int64_t off) {
+    return reinterpret_cast<T *>(h->arena + off);
+}
+
+int alloc_arena(invsim_handle *h, const Layout &lay) {
+    h->fields = lay.f;
+    h->arena_bytes = std::max<int64_t>(lay.bytes, 256);
+    hipError_t e = hipMalloc(&h->arena, (size_t)h->arena_bytes);
+    if (e != hipSuccess) return fail(h, INVSIM_ENOMEM, std::string("hipMalloc(state): ") + hipGetErrorString(e));
+    e = hipMemset(h->arena, 0, (size_t)h->arena_bytes);
+    if (e != hipSuccess) return hip_fail(h, e, "hipMemset(state)");
+    return INVSIM_OK;
+}
+
+int common_fields(invsim_handle *h, Layout &lay, int64_t &o_rng, int64_t &o_period, int64_t &o_status) {
+    o_rng = lay.add("rng", 8, 4, h->Npad);   // rows: state_hi, state_lo, inc_hi, inc_lo
+    o_period = lay.add("period", 4, 1, h->Npad);
+    o_status = lay.add("status", 4, 1, 1);
+    return 0;
+}
+
+void bind_common(invsim_handle *h, int64_t o_rng, int64_t o_period, int64_t o_status, int32_t ar) {
+    Common &c = h->cm;
+    c.N = h->N;
+    c.Npad = h->Npad;
+    c.autoreset = ar;
+    uint64_t *r = at<uint64_t>(h, o_rng);
+    c.rng.hi = r;
+    c.rng.lo = r + h->Npad;
+    c.rng.inc_hi = r + 2 * h->Npad;
+    c.rng.inc_lo = r + 3 * h->Npad;
+    c.period = at<int32_t>(h, o_period);
+    c.status = at<uint32_t>(h, o_status);
+    c.info_demand = nullptr;
+}
+
+// "done" marker: period = horizon, so NEXT_STEP autoreset resets on first step
+int init_period(invsim_handle *h, int32_t horizon) {
+    std::vector<int32_t> v((size_t)h->Npad, horizon);
+    hipError_t e = hipMemcpy(h->cm.period, v.data(), sizeof(int32_t) * h->Npad, hipMemcpyHostToDevice);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "hipMemcpy(period)");
+}
+
+int upload_tables(invsim_handle *h, const std::vector<char> &blob) {
+    if (blob.empty()) return INVSIM_OK;
+    hipError_t e = hipMalloc(&h->tables, blob.size());
+    if (e != hipSuccess) return fail(h, INVSIM_ENOMEM, "hipMalloc(tables)");
+    e = hipMemcpy(h->tables, blob.data(), blob.size(), hipMemcpyHostToDevice);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "hipMemcpy(tables)");
+}
+
+// host-side packer for read-only tables
+struct Blob {
+    std::vector<char> b;
+    template <typename T>
+    int64_t put(const T *p, size_t n) {
+        size_t off = (b.size() + 15) / 16 * 16;
+        b.resize(off + std::max<size_t>(n, 1) * sizeof(T), 0);
+        if (p && n) std::memcpy(b.data() + off, p, n * sizeof(T));
+        return (int64_t)off;
+    }
+};
+
+template <typename T>
+const T *tab(invsim_handle *h, int64_t off) {
+    return reinterpret_cast<const T *>(h->tables + off);
+}
+
+bool valid_autoreset(int32_t m) { return m >= 0 && m <= 2; }
+
+int finish_create(invsim_handle *h, invsim_handle **out, int rc) {
+    if (rc != INVSIM_OK) {
+        g_last_error = h->err;
+        invsim_destroy(h);
+        *out = nullptr;
+        return rc;
+    }
+    *out = h;
+    return INVSIM_OK;
+}
+
+int64_t pad_n(int64_t n) { return std::max<int64_t>(256, (n + 255) / 256 * 256); }
+
+}  // namespace
+
+extern "C" {
+
+int invsim_abi_version(void) { return INVSIM_ABI_VERSION; }
+
+const char *invsim_last_error(const invsim_handle *h) {
+    return h ? h->err.c_str() : g_last_error.c_str();
+}
+
+void invsim_destroy(invsim_handle *h) {
+    if (!h) return;
+    DeviceGuard g(h->device);
+    if (h->arena) (void)hipFree(h->arena);
+    if (h->tables) (void)hipFree(h->tables);
+    delete h;
+}
+
+// ------------------------------------------------------------------ Newsvendor
+int invsim_create_newsvendor(const invsim_newsvendor_spec *spec, int64_t n, int32_t device,
+                             int32_t ar, invsim_handle **out) {
+    if (!spec || !out) return fail(nullptr, INVSIM_EINVAL, "null argument");
+    if (n < 0 || n > (int64_t)1 << 31) return fail(nullptr, INVSIM_EINVAL, "n_envs out of range");
+    if (!valid_autoreset(ar)) return fail(nullptr, INVSIM_EINVAL, "bad autoreset mode");
+    const int L = std::max(0, spec->lead_time);  // newsvendor.py:65
+    if (L > 128) return fail(nullptr, INVSIM_ERANGE, "lead_time > 128 not supported");
+    if (!(spec->mu_max >= 0) || spec->mu_max > 1e18)
+        return fail(nullptr, INVSIM_EINVAL, "mu_max must be in [0, 1e18] (numpy poisson lam range)");
+    DeviceGuard g(device);
+    if (!g.ok) return fail(nullptr, INVSIM_EDEVICE, "hipSetDevice failed");
+    auto *h = new invsim_handle();
+    h->family = INVSIM_NEWSVENDOR;
+    h->device = device;
+    h->N = n;
+    h->Npad = pad_n(n);
+    h->obs_dim = L + 5;
+    h->act_dim = 1;
+    Layout lay;
+    int64_t o_rng, o_per, o_st;
+    common_fields(h, lay, o_rng, o_per, o_st);
+    int64_t o_par = lay.add("params", 8, 5, h->Npad);
+    int64_t o_pipe = lay.add("pipeline", 4, std::max(L, 1), h->Npad);
+    int rc = alloc_arena(h, lay);
+    if (rc == INVSIM_OK) {
+        bind_common(h, o_rng, o_per, o_st, ar);
+        NvParams &p = h->nv;
+        p.cm = h->cm;
+        p.L = L;
+        p.step_limit = spec->step_limit;
+        p.max_inventory = spec->max_inventory;
+        p.max_order = spec->max_order_quantity;
+        p.p_max = spec->p_max;
+        p.h_max = spec->h_max;
+        p.k_max = spec->k_max;
+        p.mu_max = spec->mu_max;
+        p.par = at<double>(h, o_par);
+        p.pipe = at<float>(h, o_pipe);
+        rc = init_period(h, std::max(spec->step_limit, 0));
+    }
+    return finish_create(h, out, rc);
+}
+
+// ------------------------------------------------------------------ InvMgmt
+int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t device, int32_t ar,
+                          invsim_handle **out) {
+    if (!s || !out) return fail(nullptr, INVSIM_EINVAL, "null argument");
+    if (n < 0 || n > (int64_t)1 << 31) return fail(nullptr, INVSIM_EINVAL, "n_envs out of range");
+    if (!valid_autoreset(ar)) return fail(nullptr, INVSIM_EINVAL, "bad autoreset mode");
+    const int m = s->num_stages, m1 = m - 1;
+    // inventory_management.py:144-167 validation
+    if (m < 2) return fail(nullptr, INVSIM_EINVAL, "Minimum number of stages is 2");
+    if (m1 > IM_MAX_M1) return fail(nullptr, INVSIM_ERANGE, "at most 9 stages supported");
+    if (s->periods <= 0) return fail(nullptr, INVSIM_EINVAL, "Number of periods must be positive");
+    if (!s->I0 || !s->unit_price || !s->unit_cost || !s->demand_cost || !s->holding_cost ||
+        !s->supply_capacity || !s->lead_time)
+        return fail(nullptr, INVSIM_EINVAL, "null parameter array");
+    for (int i = 0; i < m1; i++) {
+        if (s->I0[i] < 0) return fail(nullptr, INVSIM_EINVAL, "Initial inventory cannot be negative");
+        if (s->supply_capacity[i] <= 0) return fail(nullptr, INVSIM_EINVAL, "Supply capacities must be positive");
+        if (s->lead_time[i] < 0) return fail(nullptr, INVSIM_EINVAL, "Lead times cannot be negative");
+        if (s->lead_time[i] > 255) return fail(nullptr, INVSIM_ERANGE, "lead time > 255 not supported");
+    }
+    for (int j = 0; j < m; j++) {
+        if (!(s->unit_price[j] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Sales prices cannot be negative");
+        if (!(s->unit_cost[j] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Procurement costs cannot be negative");
+        if (!(s->demand_cost[j] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Unfulfilled demand costs cannot be negative");
+        if (!(s->holding_cost[j] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Holding costs cannot be negative");
+    }
+    if (!(s->alpha > 0 && s->alpha <= 1)) return fail(nullptr, INVSIM_EINVAL, "alpha must be in the range (0, 1]");
+    if (s->dist == 1) {
+        if (!(s->mu >= 0) || s->mu > 1e18) return fail(nullptr, INVSIM_EINVAL, "poisson mu out of range");
+    } else if (s->dist == 5) {
+        if (!s->user_D) return fail(nullptr, INVSIM_EINVAL, "User specified demand length != num periods");
+    } else if (s->dist >= 2 && s->dist <= 4) {
+        return fail(nullptr, INVSIM_EINVAL, "dist 2/3/4 (binomial/randint/geometric) not implemented on device");
+    } else {
+        return fail(nullptr, INVSIM_EINVAL, "dist must be one of 1, 2, 3, 4, 5");
+    }
+    DeviceGuard g(device);
+    if (!g.ok) return fail(nullptr, INVSIM_EDEVICE, "hipSetDevice failed");
+    auto *h = new invsim_handle();
+    h->family = INVSIM_INVMGMT;
+    h->device = device;
+    h->N = n;
+    h->Npad = pad_n(n);
+    int D = 0, sumL = 0;
+    for (int i = 0; i < m1; i++) {
+        D = std::max<int>(D, (int)s->lead_time[i]);
+        sumL += (int)s->lead_time[i];
+    }
+    h->obs_dim = m1 * (D + 1);
+    h->act_dim = m1;
+    h->im_m1 = m1;
+    h->im_backlog = s->backlog != 0;
+    Layout lay;
+    int64_t o_rng, o_per, o_st;
+    common_fields(h, lay, o_rng, o_per, o_st);
+    int64_t o_I = lay.add("I", 8, m1, h->Npad);
+    int64_t o_B = lay.add("B", 8, h->im_backlog ? m : 1, h->Npad);
+    int64_t o_R = lay.add("Rring", 8, std::max(sumL, 1), h->Npad);
+    int64_t o_A = lay.add("alog", 8, std::max(D * m1, 1), h->Npad);
+    // read-only tables: alpha**t (Python float pow == C pow), user_D
+    Blob tb;
+    std::vector<double> ap((size_t)s->periods);
+    for (int t = 0; t < s->periods; t++) ap[t] = std::pow(s->alpha, (double)t);
+    int64_t o_ap = tb.put(ap.data(), ap.size());
+    std::vector<int64_t> ud((size_t)s->periods, 0);
+    if (s->dist == 5) std::memcpy(ud.data(), s->user_D, sizeof(int64_t) * s->periods);
+    int64_t o_ud = tb.put(ud.data(), ud.size());
+    int rc = alloc_arena(h, lay);
+    if (rc == INVSIM_OK) rc = upload_tables(h, tb.b);
+    if (rc == INVSIM_OK) {
+        bind_common(h, o_rng, o_per, o_st, ar);
+        ImParams &p = h->im;
+        p.cm = h->cm;
+        p.periods = s->periods;
+        p.lt_max = D;
+        p.dist = s->dist;
+        int off = 0;
+        for (int i = 0; i < m1; i++) {
+            p.L[i] = (int32_t)s->lead_time[i];
+            p.ring_off[i] = off;
+            off += p.L[i];
+            p.c[i] = s->supply_capacity[i];
+            p.I0[i] = s->I0[i];
+        }
+        for (int j = 0; j < m; j++) {
+            p.up[j] = (double)s->unit_price[j];
+            p.uc[j] = (double)s->unit_cost[j];
+            p.hc[j] = (double)s->holding_cost[j];
+            p.kc[j] = (double)s->demand_cost[j];
+        }
+        p.pc = ptrs_const(s->dist == 1 ? s->mu : 0.0);  // host libm, as numpy
+        p.alpha_pow = tab<double>(h, o_ap);
+        p.user_D = tab<int64_t>(h, o_ud);
+        p.I = at<int64_t>(h, o_I);
+        p.B = at<int64_t>(h, o_B);
+        p.Rring = at<int64_t>(h, o_R);
+        p.alog = at<int64_t>(h, o_A);
+        rc = init_period(h, s->periods);
+    }
+    return finish_create(h, out, rc);
+}
+
+// ------------------------------------------------------------------ NetInvMgmt
+int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t device, int32_t ar,
+                             invsim_handle **out) {
+    if (!s || !out) return fail(nullptr, INVSIM_EINVAL, "null argument");
+    if (n < 0 || n > (int64_t)1 << 31) return fail(nullptr, INVSIM_EINVAL, "n_envs out of range");
+    if (!valid_autoreset(ar)) return fail(nullptr, INVSIM_EINVAL, "bad autoreset mode");
+    const int J = s->n_main, E = s->n_reorder, RL = s->n_retail;
+    if (J < 1 || E < 0 || RL < 0 || J > 64 || E > 256 || RL > 64)
+        return fail(nullptr, INVSIM_ERANGE, "topology size out of supported range");
+    if (s->num_periods <= 0) return fail(nullptr, INVSIM_EINVAL, "num_periods must be positive");
+    if (!(s->alpha > 0 && s->alpha <= 1)) return fail(nullptr, INVSIM_EINVAL, "alpha must be in (0, 1]");
+    if (!s->I0 || !s->h || !s->C || !s->o || !s->v || !s->is_factory || !s->is_retail ||
+        (E && (!s->sup || !s->pur || !s->sup_is_factory || !s->L || !s->lp || !s->lg)) ||
+        (RL && (!s->rl_node || !s->rl_p || !s->rl_b || !s->rl_lam || !s->rl_user)) ||
+        !s->succ_ptr || !s->pred_ptr)
+        return fail(nullptr, INVSIM_EINVAL, "null topology table");
+    // network_management.py:197-238 validation
+    for (int j = 0; j < J; j++) {
+        if (!(s->I0[j] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Invalid or missing I0>=0");
+        if (!(s->h[j] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Invalid or missing h>=0");
+        if (s->is_factory[j]) {
+            if (!(s->C[j] > 0)) return fail(nullptr, INVSIM_EINVAL, "Invalid or missing C>0");
+            if (!(s->o[j] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Invalid or missing o>=0");
+            if (!(s->v[j] > 0 && s->v[j] <= 1)) return fail(nullptr, INVSIM_EINVAL, "Invalid or missing v in (0, 1]");
+        }
+        if (!(s->v[j] > 0)) return fail(nullptr, INVSIM_EINVAL, "yield v must be > 0");
+    }
+    int sumL = 0;
+    for (int k = 0; k < E; k++) {
+        if (s->L[k] < 0 || s->L[k] > 255) return fail(nullptr, INVSIM_ERANGE, "Invalid or missing L>=0 (max 255)");
+        if (!(s->lp[k] >= 0) || !(s->lg[k] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Invalid or missing p/g>=0");
+        if (s->sup[k] < -1 || s->sup[k] >= J || s->pur[k] < 0 || s->pur[k] >= J)
+            return fail(nullptr, INVSIM_EINVAL, "reorder link endpoint out of range");
+        sumL += s->L[k];
+    }
+    for (int r = 0; r < RL; r++) {
+        if (s->rl_node[r] < 0 || s->rl_node[r] >= J) return fail(nullptr, INVSIM_EINVAL, "retail link node out of range");
+        if (!(s->rl_p[r] >= 0) || !(s->rl_b[r] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Invalid or missing p/b>=0");
+        if (!s->rl_user[r] && (!(s->rl_lam[r] >= 0) || s->rl_lam[r] > 1e18))
+            return fail(nullptr, INVSIM_EINVAL, "poisson lam out of range");
+        if (s->rl_user[r] && !s->user_D) return fail(nullptr, INVSIM_EINVAL, "user_D table missing");
+    }
+    const int nsucc = s->succ_ptr[J], npred = s->pred_ptr[J];
+    if (nsucc < 0 || npred < 0 || (nsucc && (!s->succ_kind || !s->succ_idx)) || (npred && !s->pred_idx))
+        return fail(nullptr, INVSIM_EINVAL, "bad adjacency tables");
+    for (int q = 0; q < nsucc; q++) {
+        if (s->succ_kind[q] == 0 ? (s->succ_idx[q] < 0 || s->succ_idx[q] >= E)
+                                 : (s->succ_idx[q] < 0 || s->succ_idx[q] >= RL))
+            return fail(nullptr, INVSIM_EINVAL, "successor index out of range");
+    }
+    for (int q = 0; q < npred; q++)
+        if (s->pred_idx[q] < 0 || s->pred_idx[q] >= E) return fail(nullptr, INVSIM_EINVAL, "predecessor index out of range");
+    DeviceGuard g(device);
+    if (!g.ok) return fail(nullptr, INVSIM_EDEVICE, "hipSetDevice failed");
+    auto *h = new invsim_handle();
+    h->family = INVSIM_NETINVMGMT;
+    h->device = device;
+    h->N = n;
+    h->Npad = pad_n(n);
+    h->obs_dim = RL + J + sumL;
+    h->act_dim = E;
+    h->demand_dim = std::max(RL, 1);
+    Layout lay;
+    int64_t o_rng, o_per, o_st;
+    common_fields(h, lay, o_rng, o_per, o_st);
+    int64_t o_X = lay.add("X", 8, J, h->Npad);
+    int64_t o_U = lay.add("U", 8, std::max(RL, 1), h->Npad);
+    int64_t o_Y = lay.add("Y", 8, std::max(E, 1), h->Npad);
+    int64_t o_R = lay.add("Rring", 8, std::max(sumL, 1), h->Npad);
+    Blob tb;
+    int64_t t_I0 = tb.put(s->I0, J), t_h = tb.put(s->h, J), t_C = tb.put(s->C, J),
+            t_o = tb.put(s->o, J), t_v = tb.put(s->v, J);
+    int64_t t_if = tb.put(s->is_factory, J), t_ir = tb.put(s->is_retail, J);
+    int64_t t_sup = tb.put(s->sup, E), t_pur = tb.put(s->pur, E), t_sf = tb.put(s->sup_is_factory, E),
+            t_L = tb.put(s->L, E), t_lp = tb.put(s->lp, E), t_lg = tb.put(s->lg, E);
+    std::vector<int32_t> roff((size_t)std::max(E, 1), 0);
+    for (int k = 0, off = 0; k < E; k++) {
+        roff[k] = off;
+        off += s->L[k];
+    }
+    int64_t t_ro = tb.put(roff.data(), roff.size());
+    int64_t t_rn = tb.put(s->rl_node, RL), t_ru = tb.put(s->rl_user, RL), t_rp = tb.put(s->rl_p, RL),
+            t_rb = tb.put(s->rl_b, RL);
+    std::vector<PtrsConst> pcs((size_t)std::max(RL, 1));
+    for (int r = 0; r < RL; r++) pcs[r] = ptrs_const(s->rl_user[r] ? 0.0 : s->rl_lam[r]);
+    int64_t t_pc = tb.put(pcs.data(), pcs.size());
+    std::vector<double> ud((size_t)std::max(RL, 1) * s->num_periods, 0.0);
+    if (s->user_D) std::memcpy(ud.data(), s->user_D, sizeof(double) * RL * s->num_periods);
+    int64_t t_ud = tb.put(ud.data(), ud.size());
+    int64_t t_sp = tb.put(s->succ_ptr, J + 1), t_sk = tb.put(s->succ_kind, nsucc),
+            t_sx = tb.put(s->succ_idx, nsucc), t_pp = tb.put(s->pred_ptr, J + 1),
+            t_px = tb.put(s->pred_idx, npred);
+    std::vector<double> ap((size_t)s->num_periods);
+    for (int t = 0; t < s->num_periods; t++) ap[t] = std::pow(s->alpha, (double)t);
+    int64_t t_ap = tb.put(ap.data(), ap.size());
+    int rc = alloc_arena(h, lay);
+    if (rc == INVSIM_OK) rc = upload_tables(h, tb.b);
+    if (rc == INVSIM_OK) {
+        bind_common(h, o_rng, o_per, o_st, ar);
+        NetParams &p = h->net;
+        p.cm = h->cm;
+        p.J = J;
+        p.E = E;
+        p.RL = RL;
+        p.T = s->num_periods;
+        p.backlog = s->backlog != 0;
+        p.sumL = sumL;
+        p.I0 = tab<double>(h, t_I0);
+        p.h = tab<double>(h, t_h);
+        p.C = tab<double>(h, t_C);
+        p.o = tab<double>(h, t_o);
+        p.v = tab<double>(h, t_v);
+        p.is_factory = tab<int32_t>(h, t_if);
+        p.is_retail = tab<int32_t>(h, t_ir);
+        p.sup = tab<int32_t>(h, t_sup);
+        p.pur = tab<int32_t>(h, t_pur);
+        p.sup_is_factory = tab<int32_t>(h, t_sf);
+        p.L = tab<int32_t>(h, t_L);
+        p.ring_off = tab<int32_t>(h, t_ro);
+        p.lp = tab<double>(h, t_lp);
+        p.lg = tab<double>(h, t_lg);
+        p.rl_node = tab<int32_t>(h, t_rn);
+        p.rl_user = tab<int32_t>(h, t_ru);
+        p.rl_p = tab<double>(h, t_rp);
+        p.rl_b = tab<double>(h, t_rb);
+        p.rl_pc = tab<PtrsConst>(h, t_pc);
+        p.user_D = tab<double>(h, t_ud);
+        p.succ_ptr = tab<int32_t>(h, t_sp);
+        p.succ_kind = tab<int32_t>(h, t_sk);
+        p.succ_idx = tab<int32_t>(h, t_sx);
+        p.pred_ptr = tab<int32_t>(h, t_pp);
+        p.pred_idx = tab<int32_t>(h, t_px);
+        p.alpha_pow = tab<double>(h, t_ap);
+        p.X = at<double>(h, o_X);
+        p.U = at<double>(h, o_U);
+        p.Y = at<double>(h, o_Y);
+        p.Rring = at<double>(h, o_R);
+        rc = init_period(h, s->num_periods);
+    }
+    return finish_create(h, out, rc);
+}
+
+// ------------------------------------------------------------------ common entry points
+int invsim_dims(const invsim_handle *h, int32_t *obs_dim, int32_t *action_dim, int32_t *demand_dim,
+                int32_t *family) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (obs_dim) *obs_dim = h->obs_dim;
+    if (action_dim) *action_dim = h->act_dim;
+    if (demand_dim) *demand_dim = h->demand_dim;
+    if (family) *family = h->family;
+    return INVSIM_OK;
+}
+
+static void sync_common(invsim_handle *h) {
+    h->nv.cm = h->cm;
+    h->im.cm = h->cm;
+    h->net.cm = h->cm;
+}
+
+int invsim_set_autoreset(invsim_handle *h, int32_t mode) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (!valid_autoreset(mode)) return fail(h, INVSIM_EINVAL, "bad autoreset mode");
+    h->cm.autoreset = mode;
+    sync_common(h);
+    return INVSIM_OK;
+}
+
+int invsim_set_info_demand(invsim_handle *h, int64_t *demand) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    h->cm.info_demand = demand;
+    sync_common(h);
+    return INVSIM_OK;
+}
+
+int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int64_t first,
+                      const uint8_t *mask, void *stream) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (first < 0) return fail(h, INVSIM_EINVAL, "first_index must be >= 0");
+    DeviceGuard g(h->device);
+    hipError_t e = seed_range_launch(h->cm, base_lo, base_hi, first, mask, (hipStream_t)stream);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_range launch");
+}
+
+int invsim_seed_words(invsim_handle *h, const uint32_t *words, const int32_t *nwords,
+                      const uint8_t *mask, void *stream) {
+    if (!h || (!words && h->N) || (!nwords && h->N)) return fail(h, INVSIM_EINVAL, "null argument");
+    DeviceGuard g(h->device);
+    hipError_t e = seed_words_launch(h->cm, words, nwords, mask, (hipStream_t)stream);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_words launch");
+}
+
+int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipSuccess;
+    switch (h->family) {
+        case INVSIM_NEWSVENDOR: e = nv_reset_launch(h->nv, mask, (float *)obs, s); break;
+        case INVSIM_INVMGMT: e = im_reset_launch(h->im, h->im_m1, h->im_backlog, mask, (int64_t *)obs, s); break;
+        case INVSIM_NETINVMGMT: e = net_reset_launch(h->net, mask, (float *)obs, s); break;
+        default: return fail(h, INVSIM_EINVAL, "bad handle family");
+    }
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "reset launch");
+}
+
+int invsim_step(invsim_handle *h, const void *actions, void *obs, double *reward, uint8_t *terminated,
+                uint8_t *truncated, void *final_obs, void *stream) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (h->N && (!actions || !obs || !reward || !terminated || !truncated))
+        return fail(h, INVSIM_EINVAL, "null output/input buffer");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipSuccess;
+    switch (h->family) {
+        case INVSIM_NEWSVENDOR:
+            e = nv_step_launch(h->nv, (const float *)actions, (float *)obs, reward, terminated,
+                               truncated, (float *)final_obs, s);
+            break;
+        case INVSIM_INVMGMT:
+            e = im_step_launch(h->im, h->im_m1, h->im_backlog, (const int64_t *)actions,
+                               (int64_t *)obs, reward, terminated, truncated, (int64_t *)final_obs, s);
+            break;
+        case INVSIM_NETINVMGMT:
+            e = net_step_launch(h->net, (const float *)actions, (float *)obs, reward, terminated,
+                                truncated, (float *)final_obs, s);
+            break;
+        default: return fail(h, INVSIM_EINVAL, "bad handle family");
+    }
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "step launch");
+}
+
+int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, double *reward,
+                   uint8_t *terminated, uint8_t *truncated, void *stream) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (K < 0) return fail(h, INVSIM_EINVAL, "K must be >= 0");
+    if (h->N && K && (!actions || !obs || !reward || !terminated || !truncated))
+        return fail(h, INVSIM_EINVAL, "null output/input buffer");
+    if (h->cm.autoreset == AR_SAME_STEP)
+        return fail(h, INVSIM_EINVAL, "rollout does not return final_obs: use NEXT_STEP or DISABLED autoreset");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipSuccess;
+    switch (h->family) {
+        case INVSIM_NEWSVENDOR:
+            e = nv_rollout_launch(h->nv, K, (const float *)actions, (float *)obs, reward, terminated, truncated, s);
+            break;
+        case INVSIM_INVMGMT:
+            e = im_rollout_launch(h->im, h->im_m1, h->im_backlog, K, (const int64_t *)actions,
+                                  (int64_t *)obs, reward, terminated, truncated, s);
+            break;
+        case INVSIM_NETINVMGMT:
+            e = net_rollout_launch(h->net, K, (const float *)actions, (float *)obs, reward, terminated, truncated, s);
+            break;
+        default: return fail(h, INVSIM_EINVAL, "bad handle family");
+    }
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "rollout launch");
+}
+
+int invsim_state_bytes(const invsim_handle *h, int64_t *bytes) {
+    if (!h || !bytes) return fail(nullptr, INVSIM_EINVAL, "null argument");
+    *bytes = h->arena_bytes;
+    return INVSIM_OK;
+}
+
+int invsim_state_field(const invsim_handle *h, int32_t idx, char name[32], int64_t *offset,
+                       int32_t *elem_bytes, int32_t *rows, int64_t *row_stride) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (idx < 0 || idx >= (int32_t)h->fields.size()) return INVSIM_ERANGE;
+    const Field &f = h->fields[idx];
+    if (name) {
+        std::memset(name, 0, 32);
+        std::strncpy(name, f.name.c_str(), 31);
+    }
+    if (offset) *offset = f.offset;
+    if (elem_bytes) *elem_bytes = f.elem;
+    if (rows) *rows = f.rows;
+    if (row_stride) *row_stride = (f.name == "status") ? 1 : h->Npad;
+    return INVSIM_OK;
+}
+
+int invsim_get_state(invsim_handle *h, void *dst, void *stream) {
+    if (!h || !dst) return fail(h, INVSIM_EINVAL, "null argument");
+    DeviceGuard g(h->device);
+    hipError_t e = hipMemcpyAsync(dst, h->arena, (size_t)h->arena_bytes, hipMemcpyDeviceToDevice,
+                                  (hipStream_t)stream);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "get_state");
+}
+
+int invsim_set_state(invsim_handle *h, const void *src, void *stream) {
+    if (!h || !src) return fail(h, INVSIM_EINVAL, "null argument");
+    DeviceGuard g(h->device);
+    hipError_t e = hipMemcpyAsync(h->arena, src, (size_t)h->arena_bytes, hipMemcpyDeviceToDevice,
+                                  (hipStream_t)stream);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "set_state");
+}
+
+}  // extern "C"

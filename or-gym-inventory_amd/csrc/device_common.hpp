@@ -1,0 +1,248 @@
+// Device-side building blocks shared by the three env kernels (gfx950).
+//
+//  * PCG64 (numpy's XSL-RR 128/64) with the 128-bit LCG step done as 64-bit
+//    halves (__umul64hi) — one per env, state SoA in HBM.
+//  * numpy SeedSequence(pool 4) -> PCG64 seeding, all 32-bit integer ops.
+//  * numpy Generator.poisson (PTRS for lam >= 10, multiplication for lam < 10)
+//    and random_loggam, restated from numpy 2.2.6 distributions.c (the
+//    third-party code the reference calls: newsvendor.py:146,
+//    inventory_management.py:172, network_management.py:125/263/540).
+//  * numpy add.reduce pairwise order for small f32/f64 sums.
+//
+// Built with -ffp-contract=off: the reference never fuses multiply-adds, and
+// Poisson acceptance tests must see the same roundings.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace invsim {
+
+constexpr uint64_t PCG_MULT_HI = 0x2360ED051FC65DA4ULL;
+constexpr uint64_t PCG_MULT_LO = 0x4385DF649FCCF645ULL;
+
+struct Pcg {
+    uint64_t hi, lo;          // 128-bit state
+    uint64_t inc_hi, inc_lo;  // 128-bit increment (odd)
+
+    __device__ __forceinline__ uint64_t next64() {
+        // state = state * MULT + inc  (mod 2^128)
+        uint64_t nlo = lo * PCG_MULT_LO;
+        uint64_t nhi = __umul64hi(lo, PCG_MULT_LO) + lo * PCG_MULT_HI + hi * PCG_MULT_LO;
+        uint64_t slo = nlo + inc_lo;
+        nhi += inc_hi + (slo < nlo ? 1ULL : 0ULL);
+        hi = nhi;
+        lo = slo;
+        uint64_t x = hi ^ lo;
+        unsigned rot = (unsigned)(hi >> 58);
+        return (x >> rot) | (x << ((64u - rot) & 63u));
+    }
+    __device__ __forceinline__ double next_double() {
+        return (double)(next64() >> 11) * (1.0 / 9007199254740992.0);
+    }
+};
+
+// ---------------------------------------------------------------- SeedSequence
+__device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t &hc) {
+    v ^= hc;
+    hc *= 0x931e8875u;
+    v *= hc;
+    v ^= v >> 16;
+    return v;
+}
+__device__ __forceinline__ uint32_t ss_mix(uint32_t x, uint32_t y) {
+    uint32_t r = 0xca01f9ddu * x - 0x4973f715u * y;
+    r ^= r >> 16;
+    return r;
+}
+
+// numpy SeedSequence(entropy words w[0..nw), nw <= 4).generate_state(4, uint64) -> PCG64 seed
+__device__ inline void seed_pcg64(const uint32_t w[4], int nw, Pcg &g) {
+    uint32_t pool[4];
+    uint32_t hc = 0x43b0d7e5u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) pool[i] = ss_hashmix(i < nw ? w[i] : 0u, hc);
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+            if (s != d) pool[d] = ss_mix(pool[d], ss_hashmix(pool[s], hc));
+    uint32_t out[8];
+    uint32_t hb = 0x8b51f9ddu;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint32_t v = pool[i & 3];
+        v ^= hb;
+        hb *= 0x58f38dedu;
+        v *= hb;
+        v ^= v >> 16;
+        out[i] = v;
+    }
+    uint64_t s_hi = (uint64_t)out[0] | ((uint64_t)out[1] << 32);
+    uint64_t s_lo = (uint64_t)out[2] | ((uint64_t)out[3] << 32);
+    uint64_t q_hi = (uint64_t)out[4] | ((uint64_t)out[5] << 32);
+    uint64_t q_lo = (uint64_t)out[6] | ((uint64_t)out[7] << 32);
+    // pcg_setseq_128_srandom_r: inc = (initseq << 1) | 1; state = 0; step; state += initstate; step
+    g.inc_hi = (q_hi << 1) | (q_lo >> 63);
+    g.inc_lo = (q_lo << 1) | 1ULL;
+    g.hi = 0;
+    g.lo = 0;
+    (void)g.next64();
+    uint64_t lo2 = g.lo + s_lo;
+    g.hi = g.hi + s_hi + (lo2 < g.lo ? 1ULL : 0ULL);
+    g.lo = lo2;
+    (void)g.next64();
+}
+
+// ---------------------------------------------------------------- Poisson
+// Constants of numpy random_poisson_ptrs that depend only on lam.  For a fixed
+// lam they are computed on the HOST with the reference platform's libm
+// (bit-identical to what numpy computes); for per-env lam (Newsvendor) on device.
+struct PtrsConst {
+    double lam, slam, loglam, b, a, invalpha, vr, log_invalpha, enlam;
+};
+
+__host__ __device__ inline PtrsConst ptrs_const(double lam) {
+    PtrsConst c;
+    c.lam = lam;
+    c.slam = sqrt(lam);
+    c.loglam = log(lam);
+    c.b = 0.931 + 2.53 * c.slam;
+    c.a = -0.059 + 0.02483 * c.b;
+    c.invalpha = 1.1239 + 1.1328 / (c.b - 3.4);
+    c.vr = 0.9277 - 3.6224 / (c.b - 2);
+    c.log_invalpha = log(c.invalpha);
+    c.enlam = exp(-lam);
+    return c;
+}
+
+__device__ inline double np_loggam(double x) {
+    const double a0 = 8.333333333333333e-02, a1 = -2.777777777777778e-03,
+                 a2 = 7.936507936507937e-04, a3 = -5.952380952380952e-04,
+                 a4 = 8.417508417508418e-04, a5 = -1.917526917526918e-03,
+                 a6 = 6.410256410256410e-03, a7 = -2.955065359477124e-02,
+                 a8 = 1.796443723688307e-01, a9 = -1.39243221690590e+00;
+    if (x == 1.0 || x == 2.0) return 0.0;
+    int64_t n = (x < 7.0) ? (int64_t)(7 - x) : 0;
+    double x0 = x + (double)n;
+    double x2 = (1.0 / x0) * (1.0 / x0);
+    double gl0 = a9;
+    gl0 *= x2; gl0 += a8;
+    gl0 *= x2; gl0 += a7;
+    gl0 *= x2; gl0 += a6;
+    gl0 *= x2; gl0 += a5;
+    gl0 *= x2; gl0 += a4;
+    gl0 *= x2; gl0 += a3;
+    gl0 *= x2; gl0 += a2;
+    gl0 *= x2; gl0 += a1;
+    gl0 *= x2; gl0 += a0;
+    const double lg2pi = 1.8378770664093453e+00;
+    double gl = gl0 / x0 + 0.5 * lg2pi + (x0 - 0.5) * log(x0) - x0;
+    if (x < 7.0) {
+        for (int64_t k = 1; k <= n; k++) {
+            gl -= log(x0 - 1.0);
+            x0 -= 1.0;
+        }
+    }
+    return gl;
+}
+
+// numpy random_poisson_ptrs (distributions.c), constants precomputed
+__device__ inline int64_t np_poisson_ptrs(Pcg &g, const PtrsConst &c) {
+    for (;;) {
+        double U = g.next_double() - 0.5;
+        double V = g.next_double();
+        double us = 0.5 - fabs(U);
+        int64_t k = (int64_t)floor((2 * c.a / us + c.b) * U + c.lam + 0.43);
+        if ((us >= 0.07) && (V <= c.vr)) return k;
+        if ((k < 0) || ((us < 0.013) && (V > us))) continue;
+        if ((log(V) + c.log_invalpha - log(c.a / (us * us) + c.b)) <=
+            (-c.lam + (double)k * c.loglam - np_loggam((double)(k + 1))))
+            return k;
+    }
+}
+
+// numpy random_poisson_mult (0 < lam < 10), enlam = exp(-lam)
+__device__ inline int64_t np_poisson_mult(Pcg &g, double enlam) {
+    int64_t X = 0;
+    double prod = 1.0;
+    for (;;) {
+        prod *= g.next_double();
+        if (prod > enlam)
+            X += 1;
+        else
+            return X;
+    }
+}
+
+// numpy random_poisson with host-precomputed constants (fixed lam)
+__device__ __forceinline__ int64_t np_poisson(Pcg &g, const PtrsConst &c) {
+    if (c.lam >= 10) return np_poisson_ptrs(g, c);
+    if (c.lam == 0) return 0;
+    return np_poisson_mult(g, c.enlam);
+}
+
+// numpy random_poisson for a per-env lam: only the branch's constants are computed
+__device__ inline int64_t np_poisson_dyn(Pcg &g, double lam) {
+    if (lam >= 10) {
+        PtrsConst c;
+        c.lam = lam;
+        c.slam = sqrt(lam);
+        c.loglam = log(lam);
+        c.b = 0.931 + 2.53 * c.slam;
+        c.a = -0.059 + 0.02483 * c.b;
+        c.invalpha = 1.1239 + 1.1328 / (c.b - 3.4);
+        c.vr = 0.9277 - 3.6224 / (c.b - 2);
+        c.log_invalpha = log(c.invalpha);
+        return np_poisson_ptrs(g, c);
+    }
+    if (lam == 0) return 0;
+    return np_poisson_mult(g, exp(-lam));
+}
+
+// ---------------------------------------------------------------- numpy sums
+// numpy add.reduce over a short contiguous 1-D array: identity 0, then
+// pairwise_sum (n < 8 sequential; n <= 128 eight accumulators + tail).
+template <typename T, class Get>
+__device__ __forceinline__ T np_sum(int n, Get get) {
+    T res;
+    if (n < 8) {
+        res = (T)0;
+        for (int i = 0; i < n; i++) res += get(i);
+    } else {
+        T r0 = get(0), r1 = get(1), r2 = get(2), r3 = get(3), r4 = get(4), r5 = get(5),
+          r6 = get(6), r7 = get(7);
+        int i = 8;
+        for (; i < n - (n % 8); i += 8) {
+            r0 += get(i + 0); r1 += get(i + 1); r2 += get(i + 2); r3 += get(i + 3);
+            r4 += get(i + 4); r5 += get(i + 5); r6 += get(i + 6); r7 += get(i + 7);
+        }
+        res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+        for (; i < n; i++) res += get(i);
+    }
+    return (T)0 + res;
+}
+
+// ---------------------------------------------------------------- RNG state I/O
+struct RngSoA {
+    uint64_t *hi, *lo, *inc_hi, *inc_lo;
+    __device__ __forceinline__ Pcg load(int64_t e) const {
+        Pcg g;
+        g.hi = hi[e];
+        g.lo = lo[e];
+        g.inc_hi = inc_hi[e];
+        g.inc_lo = inc_lo[e];
+        return g;
+    }
+    __device__ __forceinline__ void store_state(int64_t e, const Pcg &g) const {
+        hi[e] = g.hi;
+        lo[e] = g.lo;
+    }
+    __device__ __forceinline__ void store_all(int64_t e, const Pcg &g) const {
+        hi[e] = g.hi;
+        lo[e] = g.lo;
+        inc_hi[e] = g.inc_hi;
+        inc_lo[e] = g.inc_lo;
+    }
+};
+
+}  // namespace invsim

@@ -1,0 +1,296 @@
+"""Gymnasium-style VectorEnv base over libinvsim (one handle = N envs on one GPU).
+
+Mirrors ``gymnasium.vector.VectorEnv``: ``num_envs``, ``single_observation_space``,
+``single_action_space``, ``observation_space``, ``action_space``,
+``reset(seed=, options=)`` and ``step(actions)``, with torch tensors on the GPU
+in and out.  Seeding follows ``gymnasium.vector.SyncVectorEnv`` /
+SB3 ``DummyVecEnv``: ``reset(seed=s)`` seeds env i with ``s + i``
+(``benchmark_InvManagementBacklogEnv.py:264``); a list seeds env i with
+``seed[i]``; ``None`` draws fresh OS entropy the first time and afterwards
+continues the streams (gymnasium ``Env.reset(seed=None)``).
+
+Autoreset modes (``gymnasium.vector.AutoresetMode``):
+
+* ``"next_step"`` (default, gymnasium >= 1.0): the step after an env is done
+  resets it, ignoring its action, and returns the reset obs with reward 0.
+* ``"same_step"`` (SB3 VecEnv): the done step returns the reset obs, the
+  terminal obs is in ``info["final_obs"]`` (mask ``info["_final_obs"]``).
+* ``"disabled"``: the caller resets; stepping an InvMgmt/NetInvMgmt env past
+  its horizon raises IndexError as the reference does
+  (``inventory_management.py:267``).
+"""
+import os
+
+import numpy as np
+import torch
+
+from . import _capi
+from .spaces import batch_box
+
+
+def _to_device_index(device):
+    if device is None:
+        return torch.cuda.current_device()
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(f"invsim runs on a ROCm GPU (torch 'cuda' device), got {d}")
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
+def _seed_words(seeds):
+    seeds = [int(s) for s in seeds]
+    words = np.zeros((len(seeds), 4), np.uint32)
+    nw = np.zeros(len(seeds), np.int32)
+    for i, s in enumerate(seeds):
+        if s < 0 or s >= 2**128:
+            raise ValueError("seeds must be integers in [0, 2**128)")
+        k = 0
+        while True:
+            words[i, k] = s & 0xFFFFFFFF
+            k += 1
+            s >>= 32
+            if s == 0:
+                break
+        nw[i] = k
+    return words, nw
+
+
+class InvSimVectorEnv:
+    """Base class; subclasses build the spec and the single-env spaces."""
+
+    family = None
+    metadata = {"autoreset_mode": "next_step"}
+    obs_dtype = torch.float32
+    act_dtype = torch.float32
+    horizon_raises = True      # InvMgmt/Net raise past the horizon, Newsvendor keeps going
+
+    def __init__(self, num_envs, device=None, autoreset_mode="next_step", global_offset=0,
+                 record_demand=False, copy=True):
+        if not torch.cuda.is_available():
+            raise RuntimeError("invsim requires a ROCm GPU (torch.cuda.is_available() is False); "
+                               "there is no CPU fallback")
+        if autoreset_mode not in _capi.AUTORESET_MODES:
+            raise ValueError(f"autoreset_mode must be one of {sorted(_capi.AUTORESET_MODES)}")
+        self.num_envs = int(num_envs)
+        self.global_offset = int(global_offset)
+        self.device_index = _to_device_index(device)
+        self.device = torch.device("cuda", self.device_index)
+        self.autoreset_mode = autoreset_mode
+        self.copy = bool(copy)
+        self._lib = _capi.lib()
+        self._h = None
+        self._create()
+        od, ad, dd, fam = (_capi.C.c_int32() for _ in range(4))
+        _capi.check(self._lib.invsim_dims(self._h, _capi.C.byref(od), _capi.C.byref(ad),
+                                          _capi.C.byref(dd), _capi.C.byref(fam)), self._h, "dims")
+        self.obs_dim, self.action_dim, self.demand_dim = od.value, ad.value, dd.value
+        self.observation_space = batch_box(self.single_observation_space, self.num_envs)
+        self.action_space = batch_box(self.single_action_space, self.num_envs)
+        self._seeded = False
+        self._max_period = None      # host upper bound of the per-env period (disabled mode)
+        self._demand = None
+        if record_demand:
+            self._demand = torch.zeros((self.num_envs, self.demand_dim), dtype=torch.int64,
+                                       device=self.device)
+            _capi.check(self._lib.invsim_set_info_demand(self._h, self._demand.data_ptr()),
+                        self._h, "set_info_demand")
+        self._out = None
+
+    # -- subclass hooks ------------------------------------------------------
+    def _create(self):
+        raise NotImplementedError
+
+    def _horizon(self):
+        raise NotImplementedError
+
+    def _create_handle(self, fn, spec):
+        h = _capi.C.c_void_p()
+        rc = fn(_capi.C.byref(spec), self.num_envs, self.device_index,
+                _capi.AUTORESET_MODES[self.autoreset_mode], _capi.C.byref(h))
+        if rc != 0:
+            raise _capi.InvsimError(f"invsim create failed ({rc}): {_capi.last_error(None)}")
+        self._h = h
+
+    # -- helpers --------------------------------------------------------------
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _mask_ptr(self, mask):
+        if mask is None:
+            return None, None
+        m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        if m.shape != (self.num_envs,):
+            raise ValueError(f"reset_mask must have shape ({self.num_envs},)")
+        return m, m.data_ptr()
+
+    def _alloc(self, *shape, dtype):
+        return torch.empty(shape, dtype=dtype, device=self.device)
+
+    def _outputs(self):
+        N, O = self.num_envs, self.obs_dim
+        if self.copy or self._out is None:
+            self._out = (self._alloc(N, O, dtype=self.obs_dtype),
+                         self._alloc(N, dtype=torch.float64),
+                         self._alloc(N, dtype=torch.bool),
+                         self._alloc(N, dtype=torch.bool))
+        return self._out
+
+    def _actions(self, actions, lead_shape):
+        a = torch.as_tensor(actions)
+        shape = tuple(lead_shape) + (self.action_dim,)
+        if a.shape != shape:
+            if a.numel() == int(np.prod(shape)):
+                a = a.reshape(shape)
+            else:
+                raise ValueError(f"actions must have shape {shape}, got {tuple(a.shape)}")
+        return self._convert_actions(a.to(self.device)).contiguous()
+
+    def _convert_actions(self, a):
+        return a.to(self.act_dtype)
+
+    # -- public API ------------------------------------------------------------
+    def seed(self, seed=None):
+        """Re-seed the env RNGs without resetting (gymnasium seeding.np_random)."""
+        s = self._stream()
+        if seed is None:
+            ent = np.frombuffer(os.urandom(16 * self.num_envs), dtype=np.uint32).reshape(-1, 4)
+            words = torch.from_numpy(ent.copy()).to(self.device)
+            nw = torch.full((self.num_envs,), 4, dtype=torch.int32, device=self.device)
+            _capi.check(self._lib.invsim_seed_words(self._h, words.data_ptr(), nw.data_ptr(), None, s),
+                        self._h, "seed_words")
+        elif isinstance(seed, (int, np.integer)):
+            seed = int(seed)
+            if seed < 0 or seed >= 2**128:
+                raise ValueError("seed must be in [0, 2**128)")
+            _capi.check(self._lib.invsim_seed_range(self._h, seed & (2**64 - 1), seed >> 64,
+                                                    self.global_offset, None, s),
+                        self._h, "seed_range")
+        else:
+            seeds = list(seed)
+            if len(seeds) != self.num_envs:
+                raise ValueError(f"expected {self.num_envs} seeds, got {len(seeds)}")
+            w, nw = _seed_words(seeds)
+            words = torch.from_numpy(w).to(self.device)
+            nwt = torch.from_numpy(nw).to(self.device)
+            _capi.check(self._lib.invsim_seed_words(self._h, words.data_ptr(), nwt.data_ptr(), None, s),
+                        self._h, "seed_words")
+        self._seeded = True
+
+    def reset(self, *, seed=None, options=None):
+        mask = (options or {}).get("reset_mask")
+        if seed is not None or not self._seeded:
+            if mask is not None and seed is not None:
+                raise ValueError("seed together with reset_mask is not supported; seed first")
+            self.seed(seed)
+        m, mp = self._mask_ptr(mask)
+        obs = self._alloc(self.num_envs, self.obs_dim, dtype=self.obs_dtype)
+        _capi.check(self._lib.invsim_reset(self._h, mp, obs.data_ptr(), self._stream()), self._h, "reset")
+        if m is None:
+            self._max_period = 0
+        if m is not None:
+            # rows of envs that were not reset are undefined in `obs`; callers keep their own
+            pass
+        return obs, {}
+
+    def step(self, actions):
+        a = self._actions(actions, (self.num_envs,))
+        obs, rew, term, trunc = self._outputs()
+        fobs = None
+        if self.autoreset_mode == "same_step":
+            fobs = self._alloc(self.num_envs, self.obs_dim, dtype=self.obs_dtype)
+        if self.autoreset_mode == "disabled":
+            self._check_horizon(1)
+        _capi.check(self._lib.invsim_step(self._h, a.data_ptr(), obs.data_ptr(), rew.data_ptr(),
+                                          term.data_ptr(), trunc.data_ptr(),
+                                          fobs.data_ptr() if fobs is not None else None,
+                                          self._stream()), self._h, "step")
+        info = {}
+        if fobs is not None:
+            info["final_obs"] = fobs
+            info["_final_obs"] = trunc
+        if self._demand is not None:
+            info["demand"] = self._demand.clone() if self.demand_dim > 1 else self._demand[:, 0].clone()
+        return obs, rew, term, trunc, info
+
+    def rollout(self, actions):
+        """K consecutive steps in ONE kernel launch.  actions [K, N, A] ->
+        obs [K, N, O], reward [K, N], terminated [K, N], truncated [K, N].
+        Identical to K step() calls (next_step / disabled autoreset)."""
+        a = torch.as_tensor(actions)
+        K = int(a.shape[0])
+        a = self._actions(a, (K, self.num_envs))
+        N, O = self.num_envs, self.obs_dim
+        obs = self._alloc(K, N, O, dtype=self.obs_dtype)
+        rew = self._alloc(K, N, dtype=torch.float64)
+        term = self._alloc(K, N, dtype=torch.bool)
+        trunc = self._alloc(K, N, dtype=torch.bool)
+        if self.autoreset_mode == "disabled":
+            self._check_horizon(K)
+        _capi.check(self._lib.invsim_rollout(self._h, K, a.data_ptr(), obs.data_ptr(), rew.data_ptr(),
+                                             term.data_ptr(), trunc.data_ptr(), self._stream()),
+                    self._h, "rollout")
+        return obs, rew, term, trunc
+
+    def _check_horizon(self, k):
+        if not self.horizon_raises:
+            return
+        if self._max_period is None:
+            self._max_period = 0
+        if self._max_period + k > self._horizon():
+            raise IndexError(f"step past the episode horizon ({self._horizon()} periods) with "
+                             "autoreset disabled; call reset()")
+        self._max_period += k
+
+    # -- state -----------------------------------------------------------------
+    def state_bytes(self):
+        b = _capi.C.c_int64()
+        _capi.check(self._lib.invsim_state_bytes(self._h, _capi.C.byref(b)), self._h, "state_bytes")
+        return b.value
+
+    def get_state(self):
+        """Checkpoint: the whole device state (RNG streams included) as a uint8 tensor."""
+        buf = torch.empty(self.state_bytes(), dtype=torch.uint8, device=self.device)
+        _capi.check(self._lib.invsim_get_state(self._h, buf.data_ptr(), self._stream()), self._h, "get_state")
+        return buf
+
+    def set_state(self, buf):
+        buf = torch.as_tensor(buf, device=self.device).contiguous()
+        if buf.dtype != torch.uint8 or buf.numel() != self.state_bytes():
+            raise ValueError("state blob does not match this env's layout")
+        _capi.check(self._lib.invsim_set_state(self._h, buf.data_ptr(), self._stream()), self._h, "set_state")
+        self._max_period = None
+        self._seeded = True
+
+    def state_fields(self, blob=None):
+        """Decode a state blob into {name: tensor[rows, N]} views (debug / tests)."""
+        blob = self.get_state() if blob is None else blob
+        out = {}
+        i = 0
+        dt = {1: torch.uint8, 4: torch.int32, 8: torch.int64}
+        while True:
+            name = _capi.C.create_string_buffer(32)
+            off, eb, rows, stride = _capi.C.c_int64(), _capi.C.c_int32(), _capi.C.c_int32(), _capi.C.c_int64()
+            rc = self._lib.invsim_state_field(self._h, i, name, _capi.C.byref(off), _capi.C.byref(eb),
+                                              _capi.C.byref(rows), _capi.C.byref(stride))
+            if rc != 0:
+                break
+            n = rows.value * stride.value * eb.value
+            raw = blob[off.value: off.value + n].view(dt[eb.value]).view(rows.value, stride.value)
+            out[name.value.decode()] = raw[:, : self.num_envs] if stride.value > 1 else raw
+            i += 1
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            self._lib.invsim_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __repr__(self):
+        return f"{type(self).__name__}(num_envs={self.num_envs}, device={self.device})"
