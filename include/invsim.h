@@ -170,6 +170,11 @@ int invsim_step(invsim_handle *h, const void *actions, void *obs, double *reward
 int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, double *reward,
                    uint8_t *terminated, uint8_t *truncated, void *stream);
 
+/* Sticky device status word (bit 0: an env was stepped past its horizon with
+ * autoreset disabled while the period was not lock-step; such steps are not
+ * applied).  Synchronous.  clear != 0 resets it. */
+int invsim_status(invsim_handle *h, uint32_t *flags, int32_t clear);
+
 /* Optional per-step demand record (info['demand'] / D): int64 [N][demand_dim],
  * written by every subsequent step/rollout(last step) when non-NULL. */
 int invsim_set_info_demand(invsim_handle *h, int64_t *demand);

@@ -42,6 +42,11 @@ struct invsim_handle {
     NetParams net{};
     int32_t im_m1 = 0;
     bool im_backlog = false;
+    // lock-step period tracking (see kernels.hpp next_period)
+    bool t_known = true;
+    int32_t t_cur = 0;
+    int32_t horizon = 0;
+    bool past_ok = false;     // Newsvendor keeps stepping past step_limit with autoreset off
     std::string err;
 };
 
@@ -122,6 +127,9 @@ void bind_common(invsim_handle *h, int64_t o_rng, int64_t o_period, int64_t o_st
 
 // "done" marker: period = horizon, so NEXT_STEP autoreset resets on first step
 int init_period(invsim_handle *h, int32_t horizon) {
+    h->horizon = horizon;
+    h->t_known = true;
+    h->t_cur = horizon;  // "done": the first NEXT_STEP step resets
     std::vector<int32_t> v((size_t)h->Npad, horizon);
     hipError_t e = hipMemcpy(h->cm.period, v.data(), sizeof(int32_t) * h->Npad, hipMemcpyHostToDevice);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "hipMemcpy(period)");
@@ -224,6 +232,7 @@ int invsim_create_newsvendor(const invsim_newsvendor_spec *spec, int64_t n, int3
         p.mu_max = spec->mu_max;
         p.par = at<double>(h, o_par);
         p.pipe = at<float>(h, o_pipe);
+        h->past_ok = true;
         rc = init_period(h, std::max(spec->step_limit, 0));
     }
     return finish_create(h, out, rc);
@@ -279,6 +288,10 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
     }
     h->obs_dim = m1 * (D + 1);
     h->act_dim = m1;
+    if (h->obs_dim > 320) {
+        delete h;
+        return fail(nullptr, INVSIM_ERANGE, "observation length (m-1)*(max(L)+1) > 320 not supported");
+    }
     h->im_m1 = m1;
     h->im_backlog = s->backlog != 0;
     Layout lay;
@@ -431,6 +444,14 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
     if (rc == INVSIM_OK) {
         bind_common(h, o_rng, o_per, o_st, ar);
         NetParams &p = h->net;
+        p.J = J;
+        p.E = E;
+        p.RL = RL;
+        p.sumL = sumL;
+        if (net_lds_bytes(p) > 160 * 1024) rc = fail(h, INVSIM_ERANGE, "topology too large for the LDS scratch");
+    }
+    if (rc == INVSIM_OK) {
+        NetParams &p = h->net;
         p.cm = h->cm;
         p.J = J;
         p.E = E;
@@ -522,10 +543,21 @@ int invsim_seed_words(invsim_handle *h, const uint32_t *words, const int32_t *nw
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_words launch");
 }
 
+// materialise the lock-step period into the per-env row before it stops being uniform
+static int materialize_period(invsim_handle *h, hipStream_t s) {
+    if (!h->t_known) return INVSIM_OK;
+    hipError_t e = period_fill_launch(h->cm, h->t_cur, s);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "period fill");
+}
+
 int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream) {
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
+    if (mask) {
+        int rc = materialize_period(h, s);
+        if (rc != INVSIM_OK) return rc;
+    }
     hipError_t e = hipSuccess;
     switch (h->family) {
         case INVSIM_NEWSVENDOR: e = nv_reset_launch(h->nv, mask, (float *)obs, s); break;
@@ -533,7 +565,54 @@ int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream)
         case INVSIM_NETINVMGMT: e = net_reset_launch(h->net, mask, (float *)obs, s); break;
         default: return fail(h, INVSIM_EINVAL, "bad handle family");
     }
-    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "reset launch");
+    if (e != hipSuccess) return hip_fail(h, e, "reset launch");
+    if (mask) {
+        h->t_known = false;
+    } else {
+        h->t_known = true;
+        h->t_cur = 0;
+    }
+    return INVSIM_OK;
+}
+
+static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, double *reward,
+                     uint8_t *terminated, uint8_t *truncated, void *final_obs, hipStream_t s) {
+    int t_u = -1;
+    if (h->t_known) {
+        t_u = h->t_cur;
+        // DISABLED autoreset: refuse to step InvMgmt/NetInvMgmt past the horizon
+        // (the reference raises IndexError, inventory_management.py:267)
+        int t = h->t_cur;
+        for (int k = 0; k < K; k++) {
+            if (t >= h->horizon && h->cm.autoreset == AR_DISABLED && !h->past_ok)
+                return fail(h, INVSIM_ERANGE, "step past the episode horizon with autoreset disabled; reset first");
+            t = next_period(t, h->horizon, h->cm.autoreset, h->past_ok);
+        }
+    }
+    hipError_t e = hipSuccess;
+    switch (h->family) {
+        case INVSIM_NEWSVENDOR: {
+            StepIO<float, float> io{K, (const float *)actions, (float *)obs, reward, terminated, truncated, (float *)final_obs};
+            e = nv_run_launch(h->nv, t_u, io, s);
+            break;
+        }
+        case INVSIM_INVMGMT: {
+            StepIO<int64_t, int64_t> io{K, (const int64_t *)actions, (int64_t *)obs, reward, terminated, truncated,
+                                        (int64_t *)final_obs};
+            e = im_run_launch(h->im, h->im_m1, h->im_backlog, t_u, io, s);
+            break;
+        }
+        case INVSIM_NETINVMGMT: {
+            StepIO<float, float> io{K, (const float *)actions, (float *)obs, reward, terminated, truncated, (float *)final_obs};
+            e = net_run_launch(h->net, t_u, io, s);
+            break;
+        }
+        default: return fail(h, INVSIM_EINVAL, "bad handle family");
+    }
+    if (e != hipSuccess) return hip_fail(h, e, "step launch");
+    if (h->t_known)
+        for (int k = 0; k < K; k++) h->t_cur = next_period(h->t_cur, h->horizon, h->cm.autoreset, h->past_ok);
+    return INVSIM_OK;
 }
 
 int invsim_step(invsim_handle *h, const void *actions, void *obs, double *reward, uint8_t *terminated,
@@ -542,51 +621,33 @@ int invsim_step(invsim_handle *h, const void *actions, void *obs, double *reward
     if (h->N && (!actions || !obs || !reward || !terminated || !truncated))
         return fail(h, INVSIM_EINVAL, "null output/input buffer");
     DeviceGuard g(h->device);
-    hipStream_t s = (hipStream_t)stream;
-    hipError_t e = hipSuccess;
-    switch (h->family) {
-        case INVSIM_NEWSVENDOR:
-            e = nv_step_launch(h->nv, (const float *)actions, (float *)obs, reward, terminated,
-                               truncated, (float *)final_obs, s);
-            break;
-        case INVSIM_INVMGMT:
-            e = im_step_launch(h->im, h->im_m1, h->im_backlog, (const int64_t *)actions,
-                               (int64_t *)obs, reward, terminated, truncated, (int64_t *)final_obs, s);
-            break;
-        case INVSIM_NETINVMGMT:
-            e = net_step_launch(h->net, (const float *)actions, (float *)obs, reward, terminated,
-                                truncated, (float *)final_obs, s);
-            break;
-        default: return fail(h, INVSIM_EINVAL, "bad handle family");
-    }
-    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "step launch");
+    return run_steps(h, 1, actions, obs, reward, terminated, truncated,
+                     h->cm.autoreset == AR_SAME_STEP ? final_obs : nullptr, (hipStream_t)stream);
 }
 
 int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, double *reward,
                    uint8_t *terminated, uint8_t *truncated, void *stream) {
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (K < 0) return fail(h, INVSIM_EINVAL, "K must be >= 0");
-    if (h->N && K && (!actions || !obs || !reward || !terminated || !truncated))
+    if (K == 0) return INVSIM_OK;
+    if (h->N && (!actions || !obs || !reward || !terminated || !truncated))
         return fail(h, INVSIM_EINVAL, "null output/input buffer");
     if (h->cm.autoreset == AR_SAME_STEP)
         return fail(h, INVSIM_EINVAL, "rollout does not return final_obs: use NEXT_STEP or DISABLED autoreset");
     DeviceGuard g(h->device);
-    hipStream_t s = (hipStream_t)stream;
-    hipError_t e = hipSuccess;
-    switch (h->family) {
-        case INVSIM_NEWSVENDOR:
-            e = nv_rollout_launch(h->nv, K, (const float *)actions, (float *)obs, reward, terminated, truncated, s);
-            break;
-        case INVSIM_INVMGMT:
-            e = im_rollout_launch(h->im, h->im_m1, h->im_backlog, K, (const int64_t *)actions,
-                                  (int64_t *)obs, reward, terminated, truncated, s);
-            break;
-        case INVSIM_NETINVMGMT:
-            e = net_rollout_launch(h->net, K, (const float *)actions, (float *)obs, reward, terminated, truncated, s);
-            break;
-        default: return fail(h, INVSIM_EINVAL, "bad handle family");
+    return run_steps(h, K, actions, obs, reward, terminated, truncated, nullptr, (hipStream_t)stream);
+}
+
+int invsim_status(invsim_handle *h, uint32_t *flags, int32_t clear) {
+    if (!h || !flags) return fail(h, INVSIM_EINVAL, "null argument");
+    DeviceGuard g(h->device);
+    hipError_t e = hipMemcpy(flags, h->cm.status, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(h, e, "status read");
+    if (clear && *flags) {
+        e = hipMemset(h->cm.status, 0, sizeof(uint32_t));
+        if (e != hipSuccess) return hip_fail(h, e, "status clear");
     }
-    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "rollout launch");
+    return INVSIM_OK;
 }
 
 int invsim_state_bytes(const invsim_handle *h, int64_t *bytes) {
@@ -614,6 +675,8 @@ int invsim_state_field(const invsim_handle *h, int32_t idx, char name[32], int64
 int invsim_get_state(invsim_handle *h, void *dst, void *stream) {
     if (!h || !dst) return fail(h, INVSIM_EINVAL, "null argument");
     DeviceGuard g(h->device);
+    int rc = materialize_period(h, (hipStream_t)stream);  // the blob carries per-env periods
+    if (rc != INVSIM_OK) return rc;
     hipError_t e = hipMemcpyAsync(dst, h->arena, (size_t)h->arena_bytes, hipMemcpyDeviceToDevice,
                                   (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "get_state");
@@ -624,7 +687,9 @@ int invsim_set_state(invsim_handle *h, const void *src, void *stream) {
     DeviceGuard g(h->device);
     hipError_t e = hipMemcpyAsync(h->arena, src, (size_t)h->arena_bytes, hipMemcpyDeviceToDevice,
                                   (hipStream_t)stream);
-    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "set_state");
+    if (e != hipSuccess) return hip_fail(h, e, "set_state");
+    h->t_known = false;  // periods now come from the blob
+    return INVSIM_OK;
 }
 
 }  // extern "C"

@@ -37,6 +37,11 @@ seed_words_kernel(Common cm, const uint32_t *words, const int32_t *nwords, const
     cm.rng.store_all(e, g);
 }
 
+__global__ void __launch_bounds__(256) period_fill_kernel(Common cm, int32_t t) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < cm.N) cm.period[e] = t;
+}
+
 static inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 hipError_t seed_range_launch(const Common &cm, uint64_t base_lo, uint64_t base_hi, int64_t first,
@@ -52,6 +57,12 @@ hipError_t seed_words_launch(const Common &cm, const uint32_t *words, const int3
     if (cm.N == 0) return hipSuccess;
     hipLaunchKernelGGL(seed_words_kernel, dim3(grid_for(cm.N, 256)), dim3(256), 0, s, cm, words,
                        nwords, mask);
+    return hipGetLastError();
+}
+
+hipError_t period_fill_launch(const Common &cm, int32_t t, hipStream_t s) {
+    if (cm.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(period_fill_kernel, dim3(grid_for(cm.N, 256)), dim3(256), 0, s, cm, t);
     return hipGetLastError();
 }
 

@@ -77,31 +77,66 @@ struct NetParams {
     double *Rring;               // [sumL][Npad]
 };
 
+// Step I/O of one launch: K consecutive steps (K = 1 for invsim_step); row k
+// of every output is at  base + k * N * width.
+template <typename A, typename O>
+struct StepIO {
+    int K;
+    const A *act;      // [K][N][action_dim]
+    O *obs;            // [K][N][obs_dim]
+    double *rew;       // [K][N]
+    uint8_t *term;     // [K][N]
+    uint8_t *trunc;    // [K][N]
+    O *fobs;           // [N][obs_dim] final obs (SAME_STEP, K == 1), may be null
+};
+
+// Lock-step period: when every env of the handle is at the same period the host
+// knows it (t_u >= 0) and the kernels neither read nor write the per-env
+// period row; t_u = -1 means "read period[e]".  Next period after one step at t
+// (t >= horizon means "done": NEXT_STEP resets it this step).
+__host__ __device__ inline int next_period(int t, int horizon, int autoreset, bool wrap_disabled) {
+    if (t >= horizon) return (autoreset == AR_NEXT_STEP) ? 0 : t + (wrap_disabled ? 1 : 0);
+    int t1 = t + 1;
+    if (t1 >= horizon && autoreset == AR_SAME_STEP) return 0;
+    return t1;
+}
+
+constexpr int WAVE = 64;  // one-wave workgroups: LDS obs tile stored with 16-B coalesced rows
+
+// Copy `count` elements of an LDS tile to global memory, 16 B per lane.
+template <typename T>
+__device__ __forceinline__ void store_tile(const T *__restrict__ tile, T *__restrict__ dst,
+                                           int64_t count, int lane) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const int64_t bytes = count * (int64_t)sizeof(T);
+    int64_t done = 0;
+    if ((((uintptr_t)dst) & 15) == 0) {
+        const int64_t n16 = bytes >> 4;
+        const v4i *s4 = reinterpret_cast<const v4i *>(tile);
+        v4i *d4 = reinterpret_cast<v4i *>(dst);
+        for (int64_t i = lane; i < n16; i += WAVE) d4[i] = s4[i];
+        done = (n16 << 4) / (int64_t)sizeof(T);
+    }
+    for (int64_t i = done + lane; i < count; i += WAVE) dst[i] = tile[i];
+}
+
 // launchers (return hipGetLastError() of the launch)
 hipError_t seed_range_launch(const Common &cm, uint64_t base_lo, uint64_t base_hi, int64_t first,
                              const uint8_t *mask, hipStream_t s);
 hipError_t seed_words_launch(const Common &cm, const uint32_t *words, const int32_t *nwords,
                              const uint8_t *mask, hipStream_t s);
+hipError_t period_fill_launch(const Common &cm, int32_t t, hipStream_t s);
 
 hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, hipStream_t s);
-hipError_t nv_step_launch(const NvParams &p, const float *act, float *obs, double *rew,
-                          uint8_t *term, uint8_t *trunc, float *fobs, hipStream_t s);
-hipError_t nv_rollout_launch(const NvParams &p, int K, const float *act, float *obs, double *rew,
-                             uint8_t *term, uint8_t *trunc, hipStream_t s);
+hipError_t nv_run_launch(const NvParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s);
 
 hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_t *mask,
                            int64_t *obs, hipStream_t s);
-hipError_t im_step_launch(const ImParams &p, int M1, bool backlog, const int64_t *act,
-                          int64_t *obs, double *rew, uint8_t *term, uint8_t *trunc,
-                          int64_t *fobs, hipStream_t s);
-hipError_t im_rollout_launch(const ImParams &p, int M1, bool backlog, int K, const int64_t *act,
-                             int64_t *obs, double *rew, uint8_t *term, uint8_t *trunc,
-                             hipStream_t s);
+hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u,
+                         const StepIO<int64_t, int64_t> &io, hipStream_t s);
 
 hipError_t net_reset_launch(const NetParams &p, const uint8_t *mask, float *obs, hipStream_t s);
-hipError_t net_step_launch(const NetParams &p, const float *act, float *obs, double *rew,
-                           uint8_t *term, uint8_t *trunc, float *fobs, hipStream_t s);
-hipError_t net_rollout_launch(const NetParams &p, int K, const float *act, float *obs,
-                              double *rew, uint8_t *term, uint8_t *trunc, hipStream_t s);
+hipError_t net_run_launch(const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s);
+size_t net_lds_bytes(const NetParams &p);
 
 }  // namespace invsim

@@ -1,29 +1,50 @@
 // NetInvMgmtMasterEnv.step / reset (network_management.py:301-635) as a
-// topology-interpreting HIP kernel for gfx950: one thread per env, the graph
-// compiled by the host into index tables that every lane walks in lock-step
-// (all indices are wave-uniform, so table reads are scalar loads and the
-// per-env node/link scratch lives in LDS at [row][lane] — bank-conflict free).
+// topology-interpreting HIP kernel for gfx950: one thread per env, one wave
+// per workgroup, the graph compiled by the host into index tables that every
+// lane walks in lock-step (indices are wave-uniform: table reads are scalar
+// loads).  Per-env node/link values live in LDS at [row][lane] (conflict-free)
+// for the whole launch, so K steps touch HBM state once.
 //
 // Per-env HBM state (SoA rows of Npad, f64 like the reference DataFrames):
 //   X[J] on-hand inventory, U[RL] unfulfilled market demand, Y[E] pipeline,
 //   Rring[sum L] fulfilled orders per link (slot t mod L_e = R[t-L_e], the
-//   delivery arriving this period; the same ring is the obs window), period, PCG64.
+//   delivery arriving this period; the same ring is the obs window),
+//   period (only when not lock-step), PCG64.
 #include "kernels.hpp"
 
 namespace invsim {
 namespace {
 
-constexpr int NET_BS = 64;  // one wave per workgroup; LDS scratch per lane
-
 __device__ __forceinline__ double max0(double x) { return (x > 0) ? x : 0.0; }  // max(0, x)
 
-// reset (:301-332): X = I0, U = Y = 0, period 0; obs = [0(RL), I0(J), 0(sumL)]
-__device__ __forceinline__ void net_reset_one(const NetParams &P, int64_t e, float *orow) {
-    const int64_t S = P.cm.Npad;
-    for (int j = 0; j < P.J; j++) P.X[j * S + e] = P.I0[j];
-    for (int r = 0; r < P.RL; r++) P.U[r * S + e] = 0.0;
-    for (int k = 0; k < P.E; k++) P.Y[k * S + e] = 0.0;
-    P.cm.period[e] = 0;
+struct NetScratch {
+    double *X, *U, *Y;                     // persistent across the launch
+    double *cons, *arr, *Rn, *arrv, *Sr, *Dd;  // per step
+};
+
+__device__ __forceinline__ NetScratch scratch_of(const NetParams &P, double *base) {
+    NetScratch s;
+    const int J = P.J, E = P.E, RL = P.RL;
+    s.X = base;
+    s.U = s.X + J * WAVE;
+    s.Y = s.U + RL * WAVE;
+    s.cons = s.Y + E * WAVE;
+    s.arr = s.cons + J * WAVE;
+    s.Rn = s.arr + J * WAVE;
+    s.arrv = s.Rn + E * WAVE;
+    s.Sr = s.arrv + E * WAVE;
+    s.Dd = s.Sr + RL * WAVE;
+    return s;
+}
+__host__ __device__ inline int scratch_rows(int J, int E, int RL) { return 3 * J + 3 * E + 3 * RL; }
+
+#define LV(a, i) (a)[(i) * WAVE]
+
+// reset (:301-332): X = I0, U = Y = 0; obs = [0(RL), I0(J), 0(sumL)]
+__device__ __forceinline__ void net_reset_lds(const NetParams &P, NetScratch &s, float *orow) {
+    for (int j = 0; j < P.J; j++) LV(s.X, j) = P.I0[j];
+    for (int r = 0; r < P.RL; r++) LV(s.U, r) = 0.0;
+    for (int k = 0; k < P.E; k++) LV(s.Y, k) = 0.0;
     if (orow) {
         int o = 0;
         for (int r = 0; r < P.RL; r++) orow[o++] = 0.f;
@@ -32,122 +53,112 @@ __device__ __forceinline__ void net_reset_one(const NetParams &P, int64_t e, flo
     }
 }
 
-// One step (:436-635) for env e at period t < T.  lds = this lane's scratch base.
-__device__ bool net_step_one(const NetParams &P, int64_t e, Pcg &g, const float *__restrict__ arow,
-                             float *orow, double &reward, int64_t *dem, double *lds) {
+// One step (:436-635) at period t < T.  Returns truncated.
+__device__ bool net_step_lds(const NetParams &P, int64_t e, int t, Pcg &g, NetScratch &s,
+                             const float *__restrict__ arow, float *orow, double &reward, int64_t *dem) {
     const int64_t S = P.cm.Npad;
     const int J = P.J, E = P.E, RL = P.RL;
-    const int t = P.cm.period[e];
-    // LDS rows: Xs[J] cons[J] arr[J] Rn[E] arrv[E] Yn[E] Sr[RL] Un[RL]
-    double *Xs = lds, *cons = Xs + J * NET_BS, *arr = cons + J * NET_BS, *Rn = arr + J * NET_BS;
-    double *arrv = Rn + E * NET_BS, *Yn = arrv + E * NET_BS, *Sr = Yn + E * NET_BS,
-           *Un = Sr + RL * NET_BS;
-#define LV(a, i) a[(i) * NET_BS]
+    // market demand draws first (retail-link order, :536-541): RNG-only work
+    for (int r = 0; r < RL; r++) {
+        double dd;
+        if (P.rl_user[r]) {
+            const int idx = t < P.T - 1 ? t : P.T - 1;
+            dd = rint(P.user_D[(int64_t)r * P.T + idx]);       // max(0, int(round(x)))
+            if (!(dd > 0)) dd = 0.0;
+        } else {
+            const int64_t pd = np_poisson(g, P.rl_pc[r]);
+            dd = (double)(pd > 0 ? pd : 0);
+        }
+        LV(s.Dd, r) = dd;
+        if (dem) dem[e * RL + r] = (int64_t)dd;
+    }
     for (int j = 0; j < J; j++) {
-        LV(Xs, j) = P.X[j * S + e];
-        LV(cons, j) = 0.0;
-        LV(arr, j) = 0.0;
+        LV(s.cons, j) = 0.0;
+        LV(s.arr, j) = 0.0;
     }
     // 0) orders over sorted reorder links (:448-490)
     for (int k = 0; k < E; k++) {
-        const double rq = rint((double)arow[k]);          // round() half-to-even
+        const double rq = rint((double)arow[k]);           // round() half-to-even
         const double request = (rq > 0) ? rq : 0.0;        // max(0, .)
-        const int s = P.sup[k];
+        const int sp = P.sup[k];
         double f;
-        if (s < 0) {
+        if (sp < 0) {
             f = request;                                   // raw material: unlimited
         } else {
-            const double oav = max0(LV(Xs, s) - LV(cons, s));
+            const double oav = max0(LV(s.X, sp) - LV(s.cons, sp));
             double avail = oav;
             if (P.sup_is_factory[k]) {
-                const double mpi = P.v[s] * oav;
-                const double mp = (mpi < P.C[s]) ? mpi : P.C[s];   // min(C, v*avail)
+                const double mpi = P.v[sp] * oav;
+                const double mp = (mpi < P.C[sp]) ? mpi : P.C[sp];   // min(C, v*avail)
                 avail = (mp < avail) ? mp : avail;
             }
             f = (avail < request) ? avail : request;       // min(request, avail)
-            LV(cons, s) += f / P.v[s];
+            LV(s.cons, sp) += f / P.v[sp];
         }
-        LV(Rn, k) = f;
+        LV(s.Rn, k) = f;
     }
     // 1) pipeline Y[t+1] = Y[t] - R[t-L] + R[t] (:494-511); ring slot t mod L <- R[t]
     for (int k = 0; k < E; k++) {
         const int L = P.L[k];
         double a = 0.0;
         if (L == 0) {
-            a = LV(Rn, k);
+            a = LV(s.Rn, k);
         } else {
             const int64_t row = P.ring_off[k] + (int)((uint32_t)t % (uint32_t)L);
             if (t >= L) a = P.Rring[row * S + e];
-            P.Rring[row * S + e] = LV(Rn, k);
+            P.Rring[row * S + e] = LV(s.Rn, k);
         }
-        LV(arrv, k) = a;
-        const double y = P.Y[k * S + e] - a + LV(Rn, k);
-        LV(Yn, k) = y;
-        P.Y[k * S + e] = y;
+        LV(s.arrv, k) = a;
+        LV(s.Y, k) = LV(s.Y, k) - a + LV(s.Rn, k);
     }
     // arrivals in predecessor adjacency order (:516-523); X[t+1] (:528)
     for (int j = 0; j < J; j++) {
         double acc = 0.0;
-        for (int q = P.pred_ptr[j]; q < P.pred_ptr[j + 1]; q++) acc += LV(arrv, P.pred_idx[q]);
-        LV(Xs, j) = (LV(Xs, j) + acc) - LV(cons, j);
+        for (int q = P.pred_ptr[j]; q < P.pred_ptr[j + 1]; q++) acc += LV(s.arrv, P.pred_idx[q]);
+        LV(s.X, j) = (LV(s.X, j) + acc) - LV(s.cons, j);
     }
-    // 2&3) market demand and fulfilment in retail-link edge order (:536-566)
+    // 2&3) market fulfilment in retail-link edge order (:536-566)
     for (int r = 0; r < RL; r++) {
-        double dd;
-        if (P.rl_user[r]) {
-            const int idx = t < P.T - 1 ? t : P.T - 1;
-            dd = rint(P.user_D[(int64_t)r * P.T + idx]);
-            if (!(dd > 0)) dd = 0.0;
-        } else {
-            const int64_t pd = np_poisson(g, P.rl_pc[r]);
-            dd = (double)(pd > 0 ? pd : 0);
-        }
-        if (dem) dem[e * RL + r] = (int64_t)dd;
-        const double fill = dd + P.U[r * S + e];
+        const double fill = LV(s.Dd, r) + LV(s.U, r);
         const int node = P.rl_node[r];
-        const double inv = max0(LV(Xs, node));
+        const double inv = max0(LV(s.X, node));
         const double sale = (inv < fill) ? inv : fill;     // min(fill, inv)
-        LV(Xs, node) -= sale;
-        LV(Sr, r) = sale;
-        const double un = P.backlog ? fill - sale : 0.0;
-        LV(Un, r) = un;
-        P.U[r * S + e] = un;
+        LV(s.X, node) -= sale;
+        LV(s.Sr, r) = sale;
+        LV(s.U, r) = P.backlog ? fill - sale : 0.0;
     }
-    // 5) profit per main node (:578-613)
+    // 5) profit per main node (:578-613), Python sum() order = adjacency order
     double total = 0.0;
     for (int j = 0; j < J; j++) {
         double SR = 0.0, sold = 0.0;
         for (int q = P.succ_ptr[j]; q < P.succ_ptr[j + 1]; q++) {
             const int idx = P.succ_idx[q];
             const bool re = P.succ_kind[q] == 0;
-            const double sv = re ? LV(Rn, idx) : LV(Sr, idx);
+            const double sv = re ? LV(s.Rn, idx) : LV(s.Sr, idx);
             SR += (re ? P.lp[idx] : P.rl_p[idx]) * sv;
             sold += sv;
         }
         double PC = 0.0, HCp = 0.0;
-        for (int q = P.pred_ptr[j]; q < P.pred_ptr[j + 1]; q++) PC += P.lp[P.pred_idx[q]] * LV(Rn, P.pred_idx[q]);
-        const double xj = LV(Xs, j);
-        const double HC_on = P.h[j] * max0(xj);
-        for (int q = P.pred_ptr[j]; q < P.pred_ptr[j + 1]; q++) HCp += P.lg[P.pred_idx[q]] * max0(LV(Yn, P.pred_idx[q]));
+        for (int q = P.pred_ptr[j]; q < P.pred_ptr[j + 1]; q++) PC += P.lp[P.pred_idx[q]] * LV(s.Rn, P.pred_idx[q]);
+        const double HC_on = P.h[j] * max0(LV(s.X, j));
+        for (int q = P.pred_ptr[j]; q < P.pred_ptr[j + 1]; q++)
+            HCp += P.lg[P.pred_idx[q]] * max0(LV(s.Y, P.pred_idx[q]));
         const double HC = HC_on + HCp;
         double OC = 0.0;
         if (P.is_factory[j]) OC = (P.v[j] > 0) ? P.o[j] * (sold / P.v[j]) : 0.0;
         double UP = 0.0;
         if (P.is_retail[j])
             for (int q = P.succ_ptr[j]; q < P.succ_ptr[j + 1]; q++)
-                if (P.succ_kind[q] == 1) UP += P.rl_b[P.succ_idx[q]] * LV(Un, P.succ_idx[q]);
+                if (P.succ_kind[q] == 1) UP += P.rl_b[P.succ_idx[q]] * LV(s.U, P.succ_idx[q]);
         total += SR - PC - OC - HC - UP;
-        P.X[j * S + e] = xj;
     }
     reward = P.alpha_pow[t] * total;                        // :619
-    const int t1 = t + 1;
-    P.cm.period[e] = t1;
-    // obs (:334-413): U[t+1] (RL), X[t+1] (J), for each link with L>0 in sorted
-    // order the fulfilled orders R[t+1-L .. t] right-aligned, zeros before t=0
+    // obs (:334-413): U[t+1] (RL), X[t+1] (J), then for each link with L>0 in
+    // sorted order the fulfilled orders R[t+1-L .. t] right-aligned, zero before t=0
     if (orow) {
         int o = 0;
-        for (int r = 0; r < RL; r++) orow[o++] = (float)LV(Un, r);
-        for (int j = 0; j < J; j++) orow[o++] = (float)LV(Xs, j);
+        for (int r = 0; r < RL; r++) orow[o++] = (float)LV(s.U, r);
+        for (int j = 0; j < J; j++) orow[o++] = (float)LV(s.X, j);
         for (int k = 0; k < E; k++) {
             const int L = P.L[k];
             if (L == 0) continue;
@@ -160,85 +171,80 @@ __device__ bool net_step_one(const NetParams &P, int64_t e, Pcg &g, const float 
                 }
                 orow[o++] = (float)v;
             }
-            orow[o++] = (float)LV(Rn, k);
+            orow[o++] = (float)LV(s.Rn, k);
         }
     }
-#undef LV
-    return t1 >= P.T;
+    return t + 1 >= P.T;
 }
 
-__device__ __forceinline__ double *lane_scratch() {
+template <bool TU>
+__global__ void __launch_bounds__(WAVE)
+net_run_kernel(NetParams P, int t_u, StepIO<float, float> io) {
     extern __shared__ __attribute__((aligned(16))) double net_lds[];
-    return net_lds + threadIdx.x;
-}
-
-__global__ void __launch_bounds__(NET_BS)
-net_step_kernel(NetParams P, const float *__restrict__ act, float *__restrict__ obs,
-                double *__restrict__ rew, uint8_t *__restrict__ term, uint8_t *__restrict__ trunc,
-                float *__restrict__ fobs) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= P.cm.N) return;
-    const int O = P.RL + P.J + P.sumL;
-    float *orow = obs + e * O;
-    const int t = P.cm.period[e];
-    if (t >= P.T) {
-        if (P.cm.autoreset == AR_NEXT_STEP) {
-            net_reset_one(P, e, orow);
-            rew[e] = 0.0;
-            term[e] = 0;
-            trunc[e] = 0;
-        } else {
-            atomicOr(P.cm.status, 1u);
-        }
-        return;
-    }
-    Pcg g = P.cm.rng.load(e);
-    double r;
-    const bool tr = net_step_one(P, e, g, act + e * P.E, orow, r, P.cm.info_demand, lane_scratch());
-    rew[e] = r;
-    term[e] = 0;
-    trunc[e] = tr ? 1 : 0;
-    if (tr && P.cm.autoreset == AR_SAME_STEP) {
-        if (fobs)
-            for (int j = 0; j < O; j++) fobs[e * O + j] = orow[j];
-        net_reset_one(P, e, orow);
-    }
-    P.cm.rng.store_state(e, g);
-}
-
-__global__ void __launch_bounds__(NET_BS)
-net_rollout_kernel(NetParams P, int K, const float *__restrict__ act, float *__restrict__ obs,
-                   double *__restrict__ rew, uint8_t *__restrict__ term,
-                   uint8_t *__restrict__ trunc) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= P.cm.N) return;
+    const int lane = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e = e0 + lane;
     const int64_t N = P.cm.N;
+    const bool valid = e < N;
+    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
     const int O = P.RL + P.J + P.sumL;
-    Pcg g = P.cm.rng.load(e);
-    for (int k = 0; k < K; k++) {
-        const int64_t oi = (int64_t)k * N + e;
-        float *orow = obs + oi * O;
-        const int t = P.cm.period[e];
-        if (t >= P.T) {
-            if (P.cm.autoreset == AR_NEXT_STEP) {
-                net_reset_one(P, e, orow);
-                rew[oi] = 0.0;
-                term[oi] = 0;
-                trunc[oi] = 0;
-                continue;
-            }
-            atomicOr(P.cm.status, 1u);
-            break;
-        }
-        double r;
-        const bool tr = net_step_one(P, e, g, act + oi * P.E, orow, r,
-                                     k == K - 1 ? P.cm.info_demand : nullptr, lane_scratch());
-        rew[oi] = r;
-        term[oi] = 0;
-        trunc[oi] = tr ? 1 : 0;
-        if (tr && P.cm.autoreset == AR_SAME_STEP) net_reset_one(P, e, orow);
+    const int64_t S = P.cm.Npad;
+    const int rows = scratch_rows(P.J, P.E, P.RL);
+    NetScratch s = scratch_of(P, net_lds + lane);
+    float *tile = reinterpret_cast<float *>(net_lds + (int64_t)rows * WAVE);
+    float *trow = tile + (int64_t)lane * O;
+
+    Pcg g;
+    int t = t_u;
+    if (valid) {
+        g = P.cm.rng.load(e);
+        for (int j = 0; j < P.J; j++) LV(s.X, j) = P.X[j * S + e];
+        for (int r = 0; r < P.RL; r++) LV(s.U, r) = P.U[r * S + e];
+        for (int k = 0; k < P.E; k++) LV(s.Y, k) = P.Y[k * S + e];
+        if (!TU) t = P.cm.period[e];
     }
-    P.cm.rng.store_state(e, g);
+    bool fault = false;
+    for (int k = 0; k < io.K; k++) {
+        const int64_t oi = (int64_t)k * N + e;
+        if (valid) {
+            if (t >= P.T) {
+                if (P.cm.autoreset == AR_NEXT_STEP) {
+                    net_reset_lds(P, s, trow);
+                    io.rew[oi] = 0.0;
+                    io.term[oi] = 0;
+                    io.trunc[oi] = 0;
+                    t = 0;
+                } else {
+                    fault = true;
+                }
+            } else {
+                double r;
+                const bool tr = net_step_lds(P, e, t, g, s, io.act + oi * P.E, trow, r,
+                                             k == io.K - 1 ? P.cm.info_demand : nullptr);
+                io.rew[oi] = r;
+                io.term[oi] = 0;
+                io.trunc[oi] = tr ? 1 : 0;
+                t += 1;
+                if (tr && P.cm.autoreset == AR_SAME_STEP) {
+                    if (io.fobs)
+                        for (int j = 0; j < O; j++) io.fobs[e * O + j] = trow[j];
+                    net_reset_lds(P, s, trow);
+                    t = 0;
+                }
+            }
+        }
+        __syncthreads();
+        store_tile(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+        __syncthreads();
+    }
+    if (valid) {
+        P.cm.rng.store_state(e, g);
+        for (int j = 0; j < P.J; j++) P.X[j * S + e] = LV(s.X, j);
+        for (int r = 0; r < P.RL; r++) P.U[r * S + e] = LV(s.U, r);
+        for (int k = 0; k < P.E; k++) P.Y[k * S + e] = LV(s.Y, k);
+        if (!TU) P.cm.period[e] = t;
+        if (fault) atomicOr(P.cm.status, 1u);
+    }
 }
 
 __global__ void __launch_bounds__(256)
@@ -246,29 +252,40 @@ net_reset_kernel(NetParams P, const uint8_t *__restrict__ mask, float *__restric
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= P.cm.N) return;
     if (mask && !mask[e]) return;
-    net_reset_one(P, e, obs ? obs + e * (P.RL + P.J + P.sumL) : nullptr);
+    const int64_t S = P.cm.Npad;
+    for (int j = 0; j < P.J; j++) P.X[j * S + e] = P.I0[j];
+    for (int r = 0; r < P.RL; r++) P.U[r * S + e] = 0.0;
+    for (int k = 0; k < P.E; k++) P.Y[k * S + e] = 0.0;
+    P.cm.period[e] = 0;
+    if (obs) {
+        float *orow = obs + e * (P.RL + P.J + P.sumL);
+        int o = 0;
+        for (int r = 0; r < P.RL; r++) orow[o++] = 0.f;
+        for (int j = 0; j < P.J; j++) orow[o++] = (float)P.I0[j];
+        for (int q = 0; q < P.sumL; q++) orow[o++] = 0.f;
+    }
 }
 
+#undef LV
+
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
-inline size_t lds_bytes(const NetParams &p) {
-    return (size_t)(3 * p.J + 3 * p.E + 2 * p.RL) * NET_BS * sizeof(double);
-}
 
 }  // namespace
 
-hipError_t net_step_launch(const NetParams &p, const float *act, float *obs, double *rew,
-                           uint8_t *term, uint8_t *trunc, float *fobs, hipStream_t s) {
-    if (p.cm.N == 0) return hipSuccess;
-    hipLaunchKernelGGL(net_step_kernel, dim3(grid_for(p.cm.N, NET_BS)), dim3(NET_BS), lds_bytes(p),
-                       s, p, act, obs, rew, term, trunc, fobs);
-    return hipGetLastError();
+size_t net_lds_bytes(const NetParams &p) {
+    const size_t tile = (size_t)WAVE * (p.RL + p.J + p.sumL) * sizeof(float);
+    return (size_t)scratch_rows(p.J, p.E, p.RL) * WAVE * sizeof(double) + (tile + 15) / 16 * 16;
 }
 
-hipError_t net_rollout_launch(const NetParams &p, int K, const float *act, float *obs,
-                              double *rew, uint8_t *term, uint8_t *trunc, hipStream_t s) {
-    if (p.cm.N == 0 || K <= 0) return hipSuccess;
-    hipLaunchKernelGGL(net_rollout_kernel, dim3(grid_for(p.cm.N, NET_BS)), dim3(NET_BS),
-                       lds_bytes(p), s, p, K, act, obs, rew, term, trunc);
+hipError_t net_run_launch(const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s) {
+    if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
+    const size_t lds = net_lds_bytes(p);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const dim3 grid(grid_for(p.cm.N, WAVE)), block(WAVE);
+    if (t_u >= 0)
+        hipLaunchKernelGGL(net_run_kernel<true>, grid, block, lds, s, p, t_u, io);
+    else
+        hipLaunchKernelGGL(net_run_kernel<false>, grid, block, lds, s, p, t_u, io);
     return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ EXPORTS = (
     "invsim_abi_version", "invsim_last_error", "invsim_create_newsvendor",
     "invsim_create_invmgmt", "invsim_create_netinvmgmt", "invsim_destroy", "invsim_dims",
     "invsim_set_autoreset", "invsim_seed_range", "invsim_seed_words", "invsim_reset",
-    "invsim_step", "invsim_rollout", "invsim_set_info_demand", "invsim_state_bytes",
+    "invsim_step", "invsim_rollout", "invsim_status", "invsim_set_info_demand", "invsim_state_bytes",
     "invsim_state_field", "invsim_get_state", "invsim_set_state",
 )
 
@@ -76,6 +76,7 @@ def _declare(lib):
         "invsim_reset": ([H, P, P, P], C.c_int),
         "invsim_step": ([H, P, P, P, P, P, P, P], C.c_int),
         "invsim_rollout": ([H, I32, P, P, P, P, P, P], C.c_int),
+        "invsim_status": ([H, P, I32], C.c_int),
         "invsim_set_info_demand": ([H, P], C.c_int),
         "invsim_state_bytes": ([H, P], C.c_int),
         "invsim_state_field": ([H, I32, P, P, P, P, P], C.c_int),
@@ -115,7 +116,12 @@ def last_error(h=None):
     return msg.decode() if msg else ""
 
 
+INVSIM_ERANGE = -34
+
+
 def check(rc, h=None, what="invsim call"):
+    if rc == INVSIM_ERANGE and "horizon" in last_error(h):
+        raise IndexError(f"{what}: {last_error(h)}")
     if rc != 0:
         raise InvsimError(f"{what} failed ({rc}): {last_error(h)}")
     return rc

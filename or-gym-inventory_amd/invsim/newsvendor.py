@@ -18,7 +18,6 @@ class NewsvendorEnv(InvSimVectorEnv):
     family = _capi.INVSIM_NEWSVENDOR
     obs_dtype = torch.float32
     act_dtype = torch.float32
-    horizon_raises = False    # the reference keeps stepping past step_limit (newsvendor.py:190)
 
     def __init__(self, num_envs=1, device=None, lead_time=5, max_inventory=4000,
                  max_order_quantity=2000, step_limit=40, p_max=100.0, h_max=5.0, k_max=10.0,

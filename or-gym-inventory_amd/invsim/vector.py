@@ -62,7 +62,6 @@ class InvSimVectorEnv:
     metadata = {"autoreset_mode": "next_step"}
     obs_dtype = torch.float32
     act_dtype = torch.float32
-    horizon_raises = True      # InvMgmt/Net raise past the horizon, Newsvendor keeps going
 
     def __init__(self, num_envs, device=None, autoreset_mode="next_step", global_offset=0,
                  record_demand=False, copy=True):
@@ -87,7 +86,6 @@ class InvSimVectorEnv:
         self.observation_space = batch_box(self.single_observation_space, self.num_envs)
         self.action_space = batch_box(self.single_action_space, self.num_envs)
         self._seeded = False
-        self._max_period = None      # host upper bound of the per-env period (disabled mode)
         self._demand = None
         if record_demand:
             self._demand = torch.zeros((self.num_envs, self.demand_dim), dtype=torch.int64,
@@ -185,11 +183,7 @@ class InvSimVectorEnv:
         m, mp = self._mask_ptr(mask)
         obs = self._alloc(self.num_envs, self.obs_dim, dtype=self.obs_dtype)
         _capi.check(self._lib.invsim_reset(self._h, mp, obs.data_ptr(), self._stream()), self._h, "reset")
-        if m is None:
-            self._max_period = 0
-        if m is not None:
-            # rows of envs that were not reset are undefined in `obs`; callers keep their own
-            pass
+        # with a reset_mask, rows of envs that were not reset are left unwritten in `obs`
         return obs, {}
 
     def step(self, actions):
@@ -198,8 +192,6 @@ class InvSimVectorEnv:
         fobs = None
         if self.autoreset_mode == "same_step":
             fobs = self._alloc(self.num_envs, self.obs_dim, dtype=self.obs_dtype)
-        if self.autoreset_mode == "disabled":
-            self._check_horizon(1)
         _capi.check(self._lib.invsim_step(self._h, a.data_ptr(), obs.data_ptr(), rew.data_ptr(),
                                           term.data_ptr(), trunc.data_ptr(),
                                           fobs.data_ptr() if fobs is not None else None,
@@ -224,22 +216,17 @@ class InvSimVectorEnv:
         rew = self._alloc(K, N, dtype=torch.float64)
         term = self._alloc(K, N, dtype=torch.bool)
         trunc = self._alloc(K, N, dtype=torch.bool)
-        if self.autoreset_mode == "disabled":
-            self._check_horizon(K)
         _capi.check(self._lib.invsim_rollout(self._h, K, a.data_ptr(), obs.data_ptr(), rew.data_ptr(),
                                              term.data_ptr(), trunc.data_ptr(), self._stream()),
                     self._h, "rollout")
         return obs, rew, term, trunc
 
-    def _check_horizon(self, k):
-        if not self.horizon_raises:
-            return
-        if self._max_period is None:
-            self._max_period = 0
-        if self._max_period + k > self._horizon():
-            raise IndexError(f"step past the episode horizon ({self._horizon()} periods) with "
-                             "autoreset disabled; call reset()")
-        self._max_period += k
+    def status(self, clear=True):
+        """Sticky device status word (synchronous): bit 0 = an env was stepped past its
+        horizon with autoreset disabled after a masked reset (the step was not applied)."""
+        f = _capi.C.c_uint32()
+        _capi.check(self._lib.invsim_status(self._h, _capi.C.byref(f), int(clear)), self._h, "status")
+        return f.value
 
     # -- state -----------------------------------------------------------------
     def state_bytes(self):
@@ -258,7 +245,6 @@ class InvSimVectorEnv:
         if buf.dtype != torch.uint8 or buf.numel() != self.state_bytes():
             raise ValueError("state blob does not match this env's layout")
         _capi.check(self._lib.invsim_set_state(self._h, buf.data_ptr(), self._stream()), self._h, "set_state")
-        self._max_period = None
         self._seeded = True
 
     def state_fields(self, blob=None):

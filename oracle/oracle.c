@@ -331,10 +331,12 @@ void orc_nv_get_params(void *p, double *params) {
     memcpy(params, h->par, sizeof(double) * 5 * h->n);
 }
 
-/* numpy clip for float64 (_NPY_CLIP: MIN(MAX(x, lo), hi), NaN propagates) */
+/* numpy clip of a float64 (newsvendor.py:132): NaN propagates and a bound is
+ * taken only when strictly exceeded, so np.clip(-0.0, 0, hi) stays -0.0
+ * (checked against numpy in tests/test_oracle.py) */
 static double np_clip(double x, double lo, double hi) {
-    double y = isnan(x) ? x : (x > lo ? x : lo);
-    return isnan(y) ? y : (y < hi ? y : hi);
+    double y = (x < lo) ? lo : x;
+    return (y > hi) ? hi : y;
 }
 
 /* newsvendor.py:125-204 */
@@ -477,6 +479,10 @@ void orc_im_reset(void *p, int64_t *obs) {
     }
 }
 
+/* numpy int64 array arithmetic wraps around (two's complement) */
+static int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+static int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+
 /* numpy float64 -> int64 astype of an in-range value, and np.minimum(int64, f64) */
 static int64_t np_min_i64_f64(int64_t a, double b) {
     double x = (double)a;
@@ -502,7 +508,7 @@ void orc_im_step(void *p, const int64_t *action, int64_t *obs, double *reward, u
             int64_t a = action[(int64_t)i * m1 + j];
             req[j] = a > 0 ? a : 0;                                   /* :250 */
             ordreq[j] = req[j];
-            if (t >= 1) ordreq[j] = (int64_t)((uint64_t)ordreq[j] + (uint64_t)B[(int64_t)t * m + 1 + j]); /* :254-255 */
+            if (t >= 1) ordreq[j] = wadd(ordreq[j], B[(int64_t)t * m + 1 + j]); /* :254-255 */
         }
         for (int j = 0; j < m1; j++) {
             int64_t r = ordreq[j] < h->c[j] ? ordreq[j] : h->c[j];    /* :263 */
@@ -513,7 +519,7 @@ void orc_im_step(void *p, const int64_t *action, int64_t *obs, double *reward, u
         }
         for (int j = 0; j < m1; j++) {                                /* :271-277 */
             Icur[j] = I[(int64_t)t * m1 + j];
-            if (t - h->L[j] >= 0) Icur[j] += R[(int64_t)(t - h->L[j]) * m1 + j];
+            if (t - h->L[j] >= 0) Icur[j] = wadd(Icur[j], R[(int64_t)(t - h->L[j]) * m1 + j]);
         }
         int64_t d;
         if (h->dist == 5)
@@ -522,14 +528,14 @@ void orc_im_step(void *p, const int64_t *action, int64_t *obs, double *reward, u
             d = orc_poisson(rng, h->mu);                              /* :172 */
         if (d < 0) d = 0;                                             /* :280 */
         int64_t dfill = d;
-        if (t >= 1) dfill += B[(int64_t)t * m + 0];                   /* :285-286 */
+        if (t >= 1) dfill = wadd(dfill, B[(int64_t)t * m + 0]);       /* :285-286 */
         int64_t s0 = Icur[0] < dfill ? Icur[0] : dfill;               /* :288 */
-        Icur[0] -= s0;
+        Icur[0] = wsub(Icur[0], s0);
         S[0] = s0;
         for (int j = 0; j < m1; j++) S[j + 1] = Rf[j];                /* :295 */
-        for (int j = 1; j < m1; j++) Icur[j] -= Rf[j];                /* :300 (reference quirk) */
-        U[0] = dfill - s0;                                            /* :303 */
-        for (int j = 0; j < m1; j++) U[j + 1] = ordreq[j] - Rf[j];    /* :304 */
+        for (int j = 1; j < m1; j++) Icur[j] = wsub(Icur[j], Rf[j]);  /* :300 (reference quirk) */
+        U[0] = wsub(dfill, s0);                                       /* :303 */
+        for (int j = 0; j < m1; j++) U[j + 1] = wsub(ordreq[j], Rf[j]); /* :304 */
         for (int j = 0; j < m; j++) B[(int64_t)(t + 1) * m + j] = h->backlog ? U[j] : 0; /* :307-312 */
         double terms[65];
         for (int j = 0; j < m; j++) {                                 /* :315-321 */

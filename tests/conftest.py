@@ -24,11 +24,12 @@ def load_golden(name):
     return fx, cfg
 
 
-NV_GOLDENS = ["newsvendor_default", "newsvendor_capped_L9", "newsvendor_L0", "newsvendor_config1"]
+NV_GOLDENS = ["newsvendor_default", "newsvendor_capped_L9", "newsvendor_L0", "newsvendor_config1",
+              "newsvendor_edges_L0", "newsvendor_edges_L5"]
 IM_GOLDENS = ["invmgmt_backlog_default", "invmgmt_lostsales_default", "invmgmt_backlog_small_mu8",
-              "invmgmt_lostsales_9stage"]
+              "invmgmt_lostsales_9stage", "invmgmt_edges"]
 NET_GOLDENS = ["net_backlog_default", "net_lostsales_default", "net_master_truelost_alpha",
-               "net_custom_backlog"]
+               "net_custom_backlog", "net_edges"]
 
 
 def nv_kwargs(cfg):

@@ -231,7 +231,93 @@ def gen_net(name, module, cls_name, kwargs, n_env=8, n_ep=1, base_seed=6000, act
           R=R, Y=Y, P=P, reset_obs=reset_obs)
 
 
+def _tile_rows(rows, n_env, S):
+    """Edge actions: row s of `rows` (cycled) for step s, rolled by env index so
+    every env sees every edge value at a different period."""
+    rows = np.asarray(rows)
+    idx = (np.arange(S)[None, :] + np.arange(n_env)[:, None]) % len(rows)
+    return rows[idx]
+
+
+NV_EDGES = [-0.0, 0.0, 1.4e-45, -1.4e-45, 2000.0, 2000.0001, np.nan, np.inf, -np.inf, 3999.5,
+            1e38, -1e38, 0.5, 1.5, 4000.0, 123.456]
+IM_EDGES = [[2**63 - 1, 0, 0], [0, 2**63 - 1, 2**63 - 1], [-(2**63), 0, -1], [2**62, 2**62, 2**62],
+            [2**53 + 1, 0, 0], [0, 0, 0], [1, 1, 1], [100, 200, 230], [101, 201, 231], [-1, -1, -1]]
+NET_EDGES = [-0.0, 0.5, 1.5, 2.5, -0.5, 1e30, 3.4e38, -1e30, 1.4e-45, 16777217.0, 7.5, 1e7 + 0.5]
+
+
+def gen_edges():
+    """Adversarial actions at the numeric edges of each env's action handling."""
+    import inventory_management as im_ref
+    import network_management as net_ref
+    import newsvendor as nv_ref
+    import warnings
+    warnings.simplefilter("ignore")
+    for L in (0, 5):
+        n, S = 8, 16
+        acts = _tile_rows(np.array(NV_EDGES, np.float32), n, S)
+        obs = np.zeros((n, S, L + 5), np.float32)
+        rew = np.zeros((n, S))
+        trunc = np.zeros((n, S), bool)
+        dem = np.zeros((n, S), np.int64)
+        reset_obs = np.zeros((n, 1, L + 5), np.float32)
+        params = np.zeros((n, 1, 5))
+        for i in range(n):
+            env = nv_ref.NewsvendorEnv(lead_time=L, step_limit=S, mu_max=4.0 if L == 0 else 200.0)
+            reset_obs[i, 0], _ = env.reset(seed=900 + i)
+            params[i, 0] = [env.price, env.cost, env.h, env.k, env.mu]
+            for s in range(S):
+                o, r, te, tr, info = env.step(acts[i, s:s + 1])
+                obs[i, s], rew[i, s], trunc[i, s], dem[i, s] = o, r, tr, info["demand"]
+        cfg = dict(lead_time=L, step_limit=S, mu_max=4.0 if L == 0 else 200.0, n_env=n, n_ep=1,
+                   ep_len=S, base_seed=900)
+        _save(f"newsvendor_edges_L{L}", cfg, actions=acts[..., None], obs=obs, reward=rew,
+              truncated=trunc, demand=dem, reset_obs=reset_obs, params=params)
+    n, S = 8, 12
+    acts = _tile_rows(np.array(IM_EDGES, np.int64), n, S)
+    obs = np.zeros((n, S, 33), np.int64)
+    rew = np.zeros((n, S))
+    trunc = np.zeros((n, S), bool)
+    dem = np.zeros((n, S), np.int64)
+    reset_obs = np.zeros((n, 1, 33), np.int64)
+    for i in range(n):
+        env = im_ref.InvManagementBacklogEnv(periods=S)
+        reset_obs[i, 0], _ = env.reset(seed=910 + i)
+        for s in range(S):
+            o, r, te, tr, info = env.step(acts[i, s])
+            obs[i, s], rew[i, s], trunc[i, s], dem[i, s] = o, r, tr, info["demand_realized"]
+    _save("invmgmt_edges", dict(cls="InvManagementBacklogEnv", periods=S, n_env=n, n_ep=1, ep_len=S,
+                                base_seed=910, backlog=True),
+          actions=acts, obs=obs, reward=rew, truncated=trunc, demand=dem, reset_obs=reset_obs)
+    n, S = 8, 12
+    base = np.array(NET_EDGES, np.float32)
+    acts = np.stack([_tile_rows(np.roll(base, j), n, S) for j in range(11)], axis=-1)
+    O = 68
+    obs = np.zeros((n, S, O), np.float32)
+    rew = np.zeros((n, S))
+    trunc = np.zeros((n, S), bool)
+    D = np.zeros((n, S, 1))
+    reset_obs = np.zeros((n, 1, O), np.float32)
+    for i in range(n):
+        env = net_ref.NetInvMgmtBacklogEnv(num_periods=S)
+        reset_obs[i, 0], _ = env.reset(seed=920 + i)
+        for s in range(S):
+            o, r, te, tr, info = env.step(acts[i, s])
+            obs[i, s], rew[i, s], trunc[i, s] = o, r, tr
+            D[i, s] = env.D.loc[s].values
+    env0 = net_ref.NetInvMgmtBacklogEnv(num_periods=S)
+    topo = dict(main_nodes=[int(x) for x in env0.main_nodes],
+                reorder_links=[[int(a), int(b)] for a, b in env0.reorder_links],
+                retail_links=[[int(a), int(b)] for a, b in env0.retail_links], obs_dim=O, backlog=True)
+    _save("net_edges", dict(module="network_management", cls="NetInvMgmtBacklogEnv", num_periods=S,
+                            n_env=n, n_ep=1, ep_len=S, base_seed=920, topology=topo),
+          actions=acts, obs=obs, reward=rew, truncated=trunc, D=D, reset_obs=reset_obs)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "edges":
+        gen_edges()
+        return
     assert "/root/reference" in sys.path or any("reference" in p for p in sys.path), \
         "run with PYTHONPATH=tests/golden/standin:/root/reference"
     gen_rng()

@@ -1,0 +1,115 @@
+"""CPU: the C-ABI library loads and exports every symbol include/invsim.h
+declares, and the ctypes mirrors of the spec structs match the C layout.
+No compute calls (no GPU here)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "invsim.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(invsim_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from invsim import _capi
+    lib = _capi.load_library()
+    declared = _declared_functions()
+    assert len(declared) >= 18
+    missing = [f for f in declared if not hasattr(lib, f)]
+    assert not missing, missing
+    assert sorted(_capi.EXPORTS) == declared
+    assert lib.invsim_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    """The embedded HIP fat binary carries a gfx950 code object (and no other target)."""
+    from invsim import _capi
+    blob = open(_capi.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx90a", b"--gfx942", b"--gfx1100"):
+        assert other not in blob
+
+
+def test_spec_struct_layout_matches_header(tmp_path):
+    """Compile a probe against include/invsim.h and compare sizeof/offsetof with ctypes."""
+    from invsim import _capi
+    probe = tmp_path / "probe.c"
+    fields = {
+        "invsim_newsvendor_spec": (_capi.NewsvendorSpec, [f for f, _ in _capi.NewsvendorSpec._fields_]),
+        "invsim_invmgmt_spec": (_capi.InvMgmtSpec, [f for f, _ in _capi.InvMgmtSpec._fields_]),
+        "invsim_netinvmgmt_spec": (_capi.NetInvMgmtSpec, [f for f, _ in _capi.NetInvMgmtSpec._fields_]),
+    }
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    for cname, (_, names) in fields.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for n in names:
+            lines.append(f'printf("{cname} {n} %zu\\n", offsetof({cname}, {n}));')
+    lines.append("return 0;}")
+    probe.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(probe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = {}
+    for ln in out:
+        if ln:
+            a, b, c = ln.split()
+            got[(a, b)] = int(c)
+    for cname, (cls, names) in fields.items():
+        assert got[(cname, "size")] == C.sizeof(cls), cname
+        for n in names:
+            assert got[(cname, n)] == getattr(cls, n).offset, (cname, n)
+
+
+def test_create_without_gpu_fails_cleanly():
+    """No GPU in this container: create must fail with an error code, not crash."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from invsim import _capi
+    lib = _capi.load_library()
+    spec = _capi.NewsvendorSpec(5, 40, 4000.0, 2000.0, 100.0, 5.0, 10.0, 200.0, 1.0)
+    h = C.c_void_p()
+    rc = lib.invsim_create_newsvendor(C.byref(spec), 16, 0, 0, C.byref(h))
+    assert rc != 0 and not h.value
+    assert lib.invsim_last_error(None)
+
+
+def test_validation_errors_mirror_reference_asserts():
+    """Spec validation happens before any device call (inventory_management.py:144-167)."""
+    import numpy as np
+    from invsim import _capi
+    lib = _capi.load_library()
+    I0 = np.array([100, -1, 200], np.int64)
+    f4 = np.ones(4, np.float32)
+    c = np.array([100, 200, 230], np.int64)
+    L = np.array([1, 5, 10], np.int64)
+    spec = _capi.InvMgmtSpec(4, 30, 1, 1, 20.0, 0.97, I0.ctypes.data, f4.ctypes.data, f4.ctypes.data,
+                             f4.ctypes.data, f4.ctypes.data, c.ctypes.data, L.ctypes.data, None)
+    h = C.c_void_p()
+    assert lib.invsim_create_invmgmt(C.byref(spec), 8, 0, 0, C.byref(h)) == -22
+    assert b"Initial inventory cannot be negative" in lib.invsim_last_error(None)
+    I0[1] = 150
+    spec.alpha = 1.5
+    assert lib.invsim_create_invmgmt(C.byref(spec), 8, 0, 0, C.byref(h)) == -22
+    assert b"alpha" in lib.invsim_last_error(None)
+    spec.alpha = 0.97
+    spec.dist = 2
+    assert lib.invsim_create_invmgmt(C.byref(spec), 8, 0, 0, C.byref(h)) == -22
+
+
+def test_python_env_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from invsim import InvManagementBacklogEnv
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        InvManagementBacklogEnv(4)
