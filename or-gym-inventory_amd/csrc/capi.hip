@@ -175,6 +175,25 @@ int finish_create(invsim_handle *h, invsim_handle **out, int rc) {
 
 int64_t pad_n(int64_t n) { return std::max<int64_t>(256, (n + 255) / 256 * 256); }
 
+// Host table of PTRS's right-hand side  -lam + k*log(lam) - loggam(k+1)  for the
+// k that occur in practice (lam +- 12 sd), evaluated with the host libm exactly as
+// numpy evaluates it (distributions.c random_poisson_ptrs).  The device looks it
+// up instead of computing a log-gamma per rejection test; k outside falls back.
+void rhs_table(PtrsConst &c, std::vector<double> &tab) {
+    c.k0 = 0;
+    c.nk = 0;
+    c.toff = (int32_t)tab.size();
+    if (!(c.lam >= 10) || c.lam > 1e8) return;
+    const double sd = std::sqrt(c.lam);
+    const int64_t k0 = std::max<int64_t>(0, (int64_t)std::floor(c.lam - 12 * sd - 10));
+    const int64_t k1 = (int64_t)std::ceil(c.lam + 12 * sd + 40);
+    const int64_t n = std::min<int64_t>(k1 - k0, 16384);
+    for (int64_t k = k0; k < k0 + n; k++)
+        tab.push_back(-c.lam + (double)k * c.loglam - np_loggam((double)(k + 1)));
+    c.k0 = (int32_t)k0;
+    c.nk = (int32_t)n;
+}
+
 }  // namespace
 
 extern "C" {
@@ -309,11 +328,16 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
     std::vector<int64_t> ud((size_t)s->periods, 0);
     if (s->dist == 5) std::memcpy(ud.data(), s->user_D, sizeof(int64_t) * s->periods);
     int64_t o_ud = tb.put(ud.data(), ud.size());
+    PtrsConst pc = ptrs_const(s->dist == 1 ? s->mu : 0.0);  // host libm, as numpy
+    std::vector<double> rhs;
+    rhs_table(pc, rhs);
+    const int64_t o_rhs = tb.put(rhs.data(), rhs.size());
     int rc = alloc_arena(h, lay);
     if (rc == INVSIM_OK) rc = upload_tables(h, tb.b);
     if (rc == INVSIM_OK) {
         bind_common(h, o_rng, o_per, o_st, ar);
         ImParams &p = h->im;
+        p.rhs = pc.nk > 0 ? tab<double>(h, o_rhs) : nullptr;
         p.cm = h->cm;
         p.periods = s->periods;
         p.lt_max = D;
@@ -332,7 +356,7 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
             p.hc[j] = (double)s->holding_cost[j];
             p.kc[j] = (double)s->demand_cost[j];
         }
-        p.pc = ptrs_const(s->dist == 1 ? s->mu : 0.0);  // host libm, as numpy
+        p.pc = pc;
         p.alpha_pow = tab<double>(h, o_ap);
         p.user_D = tab<int64_t>(h, o_ud);
         p.I = at<int64_t>(h, o_I);
@@ -425,11 +449,22 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
         off += s->L[k];
     }
     int64_t t_ro = tb.put(roff.data(), roff.size());
+    std::vector<int32_t> woff((size_t)std::max(E, 1), 0);  // obs offset of each link's order window
+    for (int k = 0, off = RL + J; k < E; k++) {
+        woff[k] = off;
+        off += s->L[k];
+    }
+    int64_t t_wo = tb.put(woff.data(), woff.size());
     int64_t t_rn = tb.put(s->rl_node, RL), t_ru = tb.put(s->rl_user, RL), t_rp = tb.put(s->rl_p, RL),
             t_rb = tb.put(s->rl_b, RL);
     std::vector<PtrsConst> pcs((size_t)std::max(RL, 1));
-    for (int r = 0; r < RL; r++) pcs[r] = ptrs_const(s->rl_user[r] ? 0.0 : s->rl_lam[r]);
+    std::vector<double> rhs;
+    for (int r = 0; r < RL; r++) {
+        pcs[r] = ptrs_const(s->rl_user[r] ? 0.0 : s->rl_lam[r]);
+        rhs_table(pcs[r], rhs);
+    }
     int64_t t_pc = tb.put(pcs.data(), pcs.size());
+    int64_t t_rhs = tb.put(rhs.data(), rhs.size());
     std::vector<double> ud((size_t)std::max(RL, 1) * s->num_periods, 0.0);
     if (s->user_D) std::memcpy(ud.data(), s->user_D, sizeof(double) * RL * s->num_periods);
     int64_t t_ud = tb.put(ud.data(), ud.size());
@@ -478,6 +513,8 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
         p.rl_p = tab<double>(h, t_rp);
         p.rl_b = tab<double>(h, t_rb);
         p.rl_pc = tab<PtrsConst>(h, t_pc);
+        p.rhs = rhs.empty() ? nullptr : tab<double>(h, t_rhs);
+        p.win_off = tab<int32_t>(h, t_wo);
         p.user_D = tab<double>(h, t_ud);
         p.succ_ptr = tab<int32_t>(h, t_sp);
         p.succ_kind = tab<int32_t>(h, t_sk);

@@ -99,6 +99,9 @@ __device__ inline void seed_pcg64(const uint32_t w[4], int nw, Pcg &g) {
 // (bit-identical to what numpy computes); for per-env lam (Newsvendor) on device.
 struct PtrsConst {
     double lam, slam, loglam, b, a, invalpha, vr, log_invalpha, enlam;
+    double a2;        // 2 * a  (numpy evaluates 2 * a / us as (2 * a) / us)
+    int32_t k0, nk;   // host table of the PTRS right-hand side for k in [k0, k0 + nk)
+    int32_t toff, pad_;  // that table's offset in the handle's RHS table array
 };
 
 __host__ __device__ inline PtrsConst ptrs_const(double lam) {
@@ -112,10 +115,13 @@ __host__ __device__ inline PtrsConst ptrs_const(double lam) {
     c.vr = 0.9277 - 3.6224 / (c.b - 2);
     c.log_invalpha = log(c.invalpha);
     c.enlam = exp(-lam);
+    c.a2 = 2 * c.a;
+    c.k0 = 0;
+    c.nk = 0;
     return c;
 }
 
-__device__ inline double np_loggam(double x) {
+__host__ __device__ inline double np_loggam(double x) {
     const double a0 = 8.333333333333333e-02, a1 = -2.777777777777778e-03,
                  a2 = 7.936507936507937e-04, a3 = -5.952380952380952e-04,
                  a4 = 8.417508417508418e-04, a5 = -1.917526917526918e-03,
@@ -146,18 +152,45 @@ __device__ inline double np_loggam(double x) {
     return gl;
 }
 
+// PTRS right-hand side  -lam + k*log(lam) - loggam(k+1): host table when k is
+// inside it (computed with the host libm, exactly as numpy), else on device.
+__device__ __forceinline__ double ptrs_rhs(const PtrsConst &c, const double *rhs, int64_t k) {
+    if (rhs && k >= c.k0 && k < (int64_t)c.k0 + c.nk) return rhs[k - c.k0];
+    return -c.lam + (double)k * c.loglam - np_loggam((double)(k + 1));
+}
+
+// PTRS log-acceptance test  log(V) + log(invalpha) - log(a/us^2 + b) <= r,
+// decided with the f32 hardware log2 (v_log_f32) whenever the f32 estimate is
+// farther from r than a rigorous bound on its error; only near-ties (and
+// overflow) evaluate the f64 logs.  Same decision as the f64 test.
+__device__ __forceinline__ bool ptrs_log_accept(const PtrsConst &c, double V, double us, double r) {
+    constexpr double LN2 = 0.69314718055994530942;
+    const float us32 = (float)us;
+    const float x32 = (float)c.a / (us32 * us32) + (float)c.b;   // rel. error < 8 * 2^-24
+    if (x32 < 1e30f) {
+        const float l2v = __builtin_amdgcn_logf((float)V);        // log2, |err| <= 1 ulp(f32)
+        const float l2x = __builtin_amdgcn_logf(x32);
+        const double lhs = ((double)l2v * LN2 + c.log_invalpha) - (double)l2x * LN2;
+        // |f32 log2 error| <= 2^-22 |log2| (4 ulp) plus the input roundings
+        // (V: 2^-24, x: 2^-21 relative -> <= 2^-20 absolute in log2); f64 slack 2^-40
+        const double err = (fabs((double)l2v) + fabs((double)l2x)) * (LN2 * 0x1p-22) +
+                           LN2 * 0x1p-19 + (fabs(lhs) + fabs(r)) * 0x1p-40;
+        if (lhs + err < r) return true;
+        if (lhs - err > r) return false;
+    }
+    return (log(V) + c.log_invalpha - log(c.a / (us * us) + c.b)) <= r;
+}
+
 // numpy random_poisson_ptrs (distributions.c), constants precomputed
-__device__ inline int64_t np_poisson_ptrs(Pcg &g, const PtrsConst &c) {
+__device__ inline int64_t np_poisson_ptrs(Pcg &g, const PtrsConst &c, const double *rhs = nullptr) {
     for (;;) {
         double U = g.next_double() - 0.5;
         double V = g.next_double();
         double us = 0.5 - fabs(U);
-        int64_t k = (int64_t)floor((2 * c.a / us + c.b) * U + c.lam + 0.43);
+        int64_t k = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
         if ((us >= 0.07) && (V <= c.vr)) return k;
         if ((k < 0) || ((us < 0.013) && (V > us))) continue;
-        if ((log(V) + c.log_invalpha - log(c.a / (us * us) + c.b)) <=
-            (-c.lam + (double)k * c.loglam - np_loggam((double)(k + 1))))
-            return k;
+        if (ptrs_log_accept(c, V, us, ptrs_rhs(c, rhs, k))) return k;
     }
 }
 
@@ -175,8 +208,8 @@ __device__ inline int64_t np_poisson_mult(Pcg &g, double enlam) {
 }
 
 // numpy random_poisson with host-precomputed constants (fixed lam)
-__device__ __forceinline__ int64_t np_poisson(Pcg &g, const PtrsConst &c) {
-    if (c.lam >= 10) return np_poisson_ptrs(g, c);
+__device__ __forceinline__ int64_t np_poisson(Pcg &g, const PtrsConst &c, const double *rhs = nullptr) {
+    if (c.lam >= 10) return np_poisson_ptrs(g, c, rhs);
     if (c.lam == 0) return 0;
     return np_poisson_mult(g, c.enlam);
 }
@@ -193,6 +226,9 @@ __device__ inline int64_t np_poisson_dyn(Pcg &g, double lam) {
         c.invalpha = 1.1239 + 1.1328 / (c.b - 3.4);
         c.vr = 0.9277 - 3.6224 / (c.b - 2);
         c.log_invalpha = log(c.invalpha);
+        c.a2 = 2 * c.a;
+        c.k0 = 0;
+        c.nk = 0;
         return np_poisson_ptrs(g, c);
     }
     if (lam == 0) return 0;

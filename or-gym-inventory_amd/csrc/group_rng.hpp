@@ -1,0 +1,168 @@
+// Lane-group Poisson sampling: G = 4 lanes per env evaluate 4 consecutive
+// PTRS candidates (or 16 multiplication-method uniforms) of the SAME numpy
+// PCG64 stream at once, then agree on the first accepted one.  The draws,
+// the accepted value and the final stream position are exactly those of the
+// sequential numpy algorithm; only the evaluation is parallel.
+//
+// Why: at 65 536 envs a one-thread-per-env step is one wave per SIMD, and
+// PTRS's accept/reject loop (about 3 rounds per wave once 64 lanes must all
+// accept, each with the log test) is a long dependent f64 chain.  Four lanes
+// per env quadruple the waves per SIMD and finish the draw in one round
+// (all four candidates rejected: p ~ 2e-4 per env).
+//
+// Stream positions come from PCG64 jump-ahead: after n steps the LCG state is
+// A_n * s + S_n * inc  (mod 2^128) with A_n = M^n, S_n = 1 + M + ... + M^(n-1).
+#pragma once
+#include "device_common.hpp"
+
+namespace invsim {
+
+constexpr int GRP = 4;          // lanes per env
+constexpr int JUMP_MAX = 16;    // jump table covers n = 0..16
+
+struct JumpTable {
+    uint64_t a_hi[JUMP_MAX + 1], a_lo[JUMP_MAX + 1], s_hi[JUMP_MAX + 1], s_lo[JUMP_MAX + 1];
+};
+
+constexpr JumpTable make_jump_table() {
+    JumpTable t{};
+    typedef unsigned __int128 u128;
+    const u128 M = ((u128)PCG_MULT_HI << 64) | PCG_MULT_LO;
+    u128 a = 1, s = 0;
+    for (int n = 0; n <= JUMP_MAX; n++) {
+        t.a_hi[n] = (uint64_t)(a >> 64);
+        t.a_lo[n] = (uint64_t)a;
+        t.s_hi[n] = (uint64_t)(s >> 64);
+        t.s_lo[n] = (uint64_t)s;
+        s = s + a;  // S_{n+1} = S_n + M^n
+        a = a * M;
+    }
+    return t;
+}
+
+static __constant__ JumpTable c_jump = make_jump_table();
+
+// low 128 bits of (ahi:alo) * (bhi:blo)
+__device__ __forceinline__ void mul128(uint64_t ahi, uint64_t alo, uint64_t bhi, uint64_t blo,
+                                       uint64_t &rhi, uint64_t &rlo) {
+    rlo = alo * blo;
+    rhi = __umul64hi(alo, blo) + alo * bhi + ahi * blo;
+}
+
+// advance g by n LCG steps (0 <= n <= JUMP_MAX)
+__device__ __forceinline__ void pcg_jump(Pcg &g, int n) {
+    uint64_t ah, al, sh, sl;
+    mul128(c_jump.a_hi[n], c_jump.a_lo[n], g.hi, g.lo, ah, al);
+    mul128(c_jump.s_hi[n], c_jump.s_lo[n], g.inc_hi, g.inc_lo, sh, sl);
+    const uint64_t lo = al + sl;
+    g.hi = ah + sh + (lo < al ? 1ULL : 0ULL);
+    g.lo = lo;
+}
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    return (uint64_t)__shfl((long long)v, src);
+}
+
+// numpy random_poisson_ptrs, lane-group form.  `rhs` (nullable) holds the
+// host-computed right-hand side  -lam + k*log(lam) - loggam(k+1)  for k in
+// [c.k0, c.k0 + c.nk); outside it the device computes it.  All GRP lanes of an
+// env call this together with identical g and c.
+__device__ inline int64_t poisson_ptrs_grp(Pcg &g, const PtrsConst &c, const double *rhs) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int j = lane & (GRP - 1);
+    const int base = lane & ~(GRP - 1);
+    for (;;) {
+        Pcg s = g;
+        pcg_jump(s, 2 * j);                               // candidate j: draws 2j+1, 2j+2
+        const double U = s.next_double() - 0.5;
+        const double V = s.next_double();
+        const double us = 0.5 - fabs(U);
+        const int64_t k = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+        bool acc;
+        if ((us >= 0.07) && (V <= c.vr)) {
+            acc = true;
+        } else if ((k < 0) || ((us < 0.013) && (V > us))) {
+            acc = false;
+        } else {
+            acc = ptrs_log_accept(c, V, us, ptrs_rhs(c, rhs, k));
+        }
+        const uint64_t m = (uint64_t)__ballot(acc);
+        const unsigned gm = (unsigned)(m >> base) & ((1u << GRP) - 1u);
+        if (gm) {
+            const int src = base + __builtin_ctz(gm);
+            g.hi = shfl_u64(s.hi, src);
+            g.lo = shfl_u64(s.lo, src);
+            return (int64_t)shfl_u64((uint64_t)k, src);
+        }
+        g.hi = shfl_u64(s.hi, base + GRP - 1);            // all rejected: continue after 2*GRP draws
+        g.lo = shfl_u64(s.lo, base + GRP - 1);
+    }
+}
+
+// numpy random_poisson_mult (0 < lam < 10), lane-group form: each lane draws 4
+// consecutive uniforms, every lane forms the sequential product in stream order.
+__device__ inline int64_t poisson_mult_grp(Pcg &g, double enlam) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int j = lane & (GRP - 1);
+    const int base = lane & ~(GRP - 1);
+    constexpr int R = 4;                                   // uniforms per lane per round
+    int64_t X = 0;
+    double prod = 1.0;
+    for (;;) {
+        Pcg s = g;
+        pcg_jump(s, R * j);
+        double u[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) u[q] = s.next_double();
+        int stop = -1;
+#pragma unroll
+        for (int src = 0; src < GRP; src++) {
+#pragma unroll
+            for (int q = 0; q < R; q++) {
+                const double uq = __shfl(u[q], base + src);
+                if (stop < 0) {
+                    prod *= uq;
+                    if (prod > enlam)
+                        X += 1;
+                    else
+                        stop = src * R + q;
+                }
+            }
+        }
+        if (stop >= 0) {
+            pcg_jump(g, stop + 1);                          // uniforms consumed: stop + 1
+            return X;
+        }
+        pcg_jump(g, R * GRP);
+    }
+}
+
+// numpy random_poisson with fixed-lam constants (host libm) and optional RHS table
+__device__ __forceinline__ int64_t np_poisson_grp(Pcg &g, const PtrsConst &c, const double *rhs) {
+    if (c.lam >= 10) return poisson_ptrs_grp(g, c, rhs);
+    if (c.lam == 0) return 0;
+    return poisson_mult_grp(g, c.enlam);
+}
+
+// numpy random_poisson for a per-env lam (Newsvendor): constants on device
+__device__ inline int64_t np_poisson_dyn_grp(Pcg &g, double lam) {
+    if (lam >= 10) {
+        PtrsConst c;
+        c.lam = lam;
+        c.slam = sqrt(lam);
+        c.loglam = log(lam);
+        c.b = 0.931 + 2.53 * c.slam;
+        c.a = -0.059 + 0.02483 * c.b;
+        c.invalpha = 1.1239 + 1.1328 / (c.b - 3.4);
+        c.vr = 0.9277 - 3.6224 / (c.b - 2);
+        c.log_invalpha = log(c.invalpha);
+        c.a2 = 2 * c.a;
+        c.k0 = 0;
+        c.nk = 0;
+        return poisson_ptrs_grp(g, c, nullptr);
+    }
+    if (lam == 0) return 0;
+    return poisson_mult_grp(g, exp(-lam));
+}
+
+}  // namespace invsim

@@ -1,7 +1,13 @@
 // InvManagementMasterEnv.step / reset (inventory_management.py:186-352) as
-// HIP kernels for gfx950: one thread per env, one wave per workgroup,
-// templated on M1 = m-1 inventory stages (register arrays), backlog vs lost
-// sales, and whether the episode period is lock-step uniform (TU).
+// HIP kernels for gfx950, templated on M1 = m-1 inventory stages (register
+// arrays), backlog vs lost sales, and whether the episode period is lock-step
+// uniform (TU).
+//
+// Work layout: one wave = 16 envs x 4 lanes (group_rng.hpp).  The 4 lanes of
+// an env run the (cheap, integer) dynamics redundantly, evaluate 4 Poisson
+// candidates in parallel, split the observation-window copy, and only the
+// group leader writes state.  Observation rows are assembled in an LDS tile
+// and written with 16-byte coalesced stores.
 //
 // Per-env HBM state (SoA rows of Npad, int64 like the reference):
 //   I[M1]            on-hand inventory at the start of the period   (:203)
@@ -15,12 +21,13 @@
 // reference's zeroed history would be, so reset writes only I, B, period.
 //
 // A launch runs K >= 1 consecutive steps (invsim_step: K = 1; invsim_rollout:
-// K) with PCG64, I, B and the period in registers.  Each step's obs rows are
-// assembled in an LDS tile and written with 16-byte coalesced stores.
+// K) with PCG64, I, B and the period in registers.
 #include "kernels.hpp"
 
 namespace invsim {
 namespace {
+
+constexpr int IM_WLANE = (36 + LPE - 1) / LPE;  // obs-window entries per lane kept in registers (27 needed at D=10, M1=3)
 
 // numpy int64 array arithmetic wraps around (two's complement)
 __device__ __forceinline__ int64_t wrap_add(int64_t a, int64_t b) {
@@ -43,71 +50,90 @@ struct ImState {
     int64_t B[M1 + 1];
 };
 
-// reset (:197-220): I = I0, B = 0, period 0; obs = [I0, 0...]
+// reset (:197-220): I = I0, B = 0; obs row = [I0, 0...] (lane j of the group
+// writes every 4th element)
 template <int M1, bool BACKLOG>
-__device__ __forceinline__ void im_reset_regs(const ImParams &P, ImState<M1, BACKLOG> &s, int64_t *orow) {
+__device__ __forceinline__ void im_reset_regs(const ImParams &P, ImState<M1, BACKLOG> &s,
+                                              int64_t *orow, int j) {
 #pragma unroll
     for (int i = 0; i < M1; i++) s.I[i] = P.I0[i];
 #pragma unroll
-    for (int j = 0; j <= M1; j++) s.B[j] = 0;
+    for (int q = 0; q <= M1; q++) s.B[q] = 0;
     if (orow) {
         const int O = M1 * (P.lt_max + 1);
-#pragma unroll
-        for (int i = 0; i < M1; i++) orow[i] = P.I0[i];
-        for (int j = M1; j < O; j++) orow[j] = 0;
+        for (int q = j; q < O; q += LPE) orow[q] = (q < M1) ? P.I0[q] : 0;
     }
 }
 
 // One step (:224-352) at period t < periods.  Returns truncated.
 template <int M1, bool BACKLOG>
-__device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int t,
+__device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int j, int t,
                                              ImState<M1, BACKLOG> &s,
                                              const int64_t *__restrict__ arow, int64_t *orow,
-                                             double &reward, int64_t *dem) {
+                                             double &reward, int64_t &dem_out) {
     const int64_t S = P.cm.Npad;
     const int D = P.lt_max;
-    // demand first: it depends only on the RNG stream, so its arithmetic
-    // overlaps the loads below (:172, :280)
-    int64_t d = (P.dist == 5) ? P.user_D[t] : np_poisson(s.g, P.pc);
-    if (d < 0) d = 0;
+    const bool leader = j == 0;
+    // Phase A: every load of the step up front (actions, arrivals, this lane's
+    // share of the observation window) so the latency overlaps the demand draw
     int64_t req[M1], ordreq[M1], R[M1], arr[M1];
 #pragma unroll
-    for (int i = 0; i < M1; i++) {
-        const int64_t a = arow[i];
-        req[i] = a > 0 ? a : 0;                                     // :250
-    }
-    // arrivals R[t - L_i] (:271-277) from the stage rings
+    for (int i = 0; i < M1; i++) req[i] = arow[i];
 #pragma unroll
-    for (int i = 0; i < M1; i++) {
+    for (int i = 0; i < M1; i++) {                                  // arrivals R[t-L_i] (:271-277)
         const int L = P.L[i];
         arr[i] = 0;
         if (L > 0 && t >= L)
             arr[i] = P.Rring[(int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e];
     }
-    // observation window rows t+1-n .. t-1 from the action_log ring (:380)
+    // window rows t+1-n .. t-1 of the action_log ring (:380): nw entries, lane j
+    // takes entries q = j, j+4, ...
     const int t1 = t + 1;
     const int n = D > 0 ? (t1 < D ? t1 : D) : 0;
-    if (orow && D > 0) {
-        int slot = (int)((uint32_t)(t1 - n) % (uint32_t)D);
-        int64_t *w = orow + M1;
-        for (int r = 0; r + 1 < n; r++) {
+    const int nw = n > 0 ? (n - 1) * M1 : 0;
+    const int slot0 = D > 0 ? (int)((uint32_t)(t1 - n) % (uint32_t)D) : 0;
+    auto wsrc = [&](int q) -> const int64_t * {
+        const int r = q / M1, i = q - r * M1;
+        int slot = slot0 + r;
+        slot = slot >= D ? slot - D : slot;
+        return P.alog + ((int64_t)slot * M1 + i) * S + e;
+    };
+    const bool wreg = orow && nw <= IM_WLANE * LPE;
+    int64_t wv[IM_WLANE];
+#ifndef INVSIM_ABL_NO_WINDOW
+    if (wreg) {
 #pragma unroll
-            for (int i = 0; i < M1; i++) w[r * M1 + i] = P.alog[((int64_t)slot * M1 + i) * S + e];
-            slot = (slot + 1 == D) ? 0 : slot + 1;
+        for (int u = 0; u < IM_WLANE; u++) {
+            const int q = j + u * LPE;
+            wv[u] = (q < nw) ? *wsrc(q) : 0;
         }
     }
+#endif
+    // Phase B: demand, a function of the RNG stream only (:172, :280)
+#ifdef INVSIM_ABL_NO_POISSON  // profiling ablation build only (wrong results)
+    int64_t d = 20 + (int64_t)(s.g.lo & 3);
+#else
+    int64_t d = (P.dist == 5) ? P.user_D[t] : env_poisson(s.g, P.pc, P.rhs);
+#endif
+    if (d < 0) d = 0;
+    // Phase C: dynamics (identical in the 4 lanes)
+#pragma unroll
+    for (int i = 0; i < M1; i++) req[i] = req[i] > 0 ? req[i] : 0;  // :250
 #pragma unroll
     for (int i = 0; i < M1; i++) {
         ordreq[i] = wrap_add(req[i], s.B[i + 1]);                   // :253-255
         const int64_t r = ordreq[i] < P.c[i] ? ordreq[i] : P.c[i];  // :263
-        R[i] = (i + 1 < M1) ? min_via_f64(r, s.I[i + 1]) : r;       // :260-265 (last: inf)
+        // :260-265 np.minimum(., [I[t,1:], inf]) in float64, then astype(int64):
+        // the last stage's cap is +inf but the f64 round trip still rounds |r| > 2^53
+        R[i] = (i + 1 < M1) ? min_via_f64(r, s.I[i + 1]) : (int64_t)(double)r;
     }
     int64_t Icur[M1];
 #pragma unroll
     for (int i = 0; i < M1; i++) {
         const int L = P.L[i];
         Icur[i] = wrap_add(s.I[i], L == 0 ? R[i] : arr[i]);
-        if (L > 0) P.Rring[(int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e] = R[i];
+        if (L > 0 && leader)
+            P.Rring[(int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e] = R[i];
     }
     const int64_t dfill = wrap_add(d, s.B[0]);                      // :284-286
     const int64_t s0 = Icur[0] < dfill ? Icur[0] : dfill;           // :288
@@ -123,30 +149,45 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int t
     for (int i = 0; i < M1; i++) U[i + 1] = wrap_sub(ordreq[i], R[i]); // :304
     double term[M1 + 1];                                            // :315-321
 #pragma unroll
-    for (int j = 0; j <= M1; j++) {
-        const double Sj = (double)Sv[j];
-        const int64_t inv = (j < M1) ? Icur[j] : 0;
-        const double hold = P.hc[j] * (double)(inv > 0 ? inv : 0);
-        term[j] = ((P.up[j] * Sj - P.uc[j] * Sj) - hold) - P.kc[j] * (double)U[j];
+    for (int q = 0; q <= M1; q++) {
+        const double Sj = (double)Sv[q];
+        const int64_t inv = (q < M1) ? Icur[q] : 0;
+        const double hold = P.hc[q] * (double)(inv > 0 ? inv : 0);
+        term[q] = ((P.up[q] * Sj - P.uc[q] * Sj) - hold) - P.kc[q] * (double)U[q];
     }
-    const double profit = np_sum<double>(M1 + 1, [&](int j) { return term[j]; });
+    const double profit = np_sum<double>(M1 + 1, [&](int q) { return term[q]; });
     reward = P.alpha_pow[t] * profit;                               // :322
 #pragma unroll
     for (int i = 0; i < M1; i++) s.I[i] = Icur[i];                  // :326
 #pragma unroll
-    for (int j = 0; j <= M1; j++) s.B[j] = BACKLOG ? U[j] : 0;      // :307-312
-    if (dem) dem[e] = d;
+    for (int q = 0; q <= M1; q++) s.B[q] = BACKLOG ? U[q] : 0;      // :307-312
+    dem_out = d;
     if (orow) {                                                     // :354-391
+        int64_t *w = orow + M1;
+        if (leader) {
 #pragma unroll
-        for (int i = 0; i < M1; i++) orow[i] = Icur[i];
+            for (int i = 0; i < M1; i++) orow[i] = Icur[i];
+            if (D > 0) {
+#pragma unroll
+                for (int i = 0; i < M1; i++) w[(n - 1) * M1 + i] = req[i];
+            }
+        }
         if (D > 0) {
-            int64_t *w = orow + M1;
+            if (wreg) {
 #pragma unroll
-            for (int i = 0; i < M1; i++) w[(n - 1) * M1 + i] = req[i];
-            for (int j = n * M1; j < D * M1; j++) w[j] = 0;
+                for (int u = 0; u < IM_WLANE; u++) {
+                    const int q = j + u * LPE;
+                    if (q < nw) w[q] = wv[u];
+                }
+            } else {
+#ifndef INVSIM_ABL_NO_WINDOW
+                for (int q = j; q < nw; q += LPE) w[q] = *wsrc(q);
+#endif
+            }
+            for (int q = n * M1 + j; q < D * M1; q += LPE) w[q] = 0;
         }
     }
-    if (D > 0) {
+    if (D > 0 && leader) {
         const int wslot = (int)((uint32_t)t % (uint32_t)D);
 #pragma unroll
         for (int i = 0; i < M1; i++) P.alog[((int64_t)wslot * M1 + i) * S + e] = req[i];  // :268
@@ -159,14 +200,16 @@ __global__ void __launch_bounds__(WAVE)
 im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io) {
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
     const int lane = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
-    const int64_t e = e0 + lane;
+    const int j = lane & (LPE - 1);
+    const bool leader = j == 0;
+    const int64_t e0 = (int64_t)blockIdx.x * EPW;
+    const int64_t e = e0 + (lane / LPE);
     const int64_t N = P.cm.N;
     const bool valid = e < N;
-    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
+    const int nvalid = (int)((N - e0) < EPW ? (N - e0) : EPW);
     const int O = M1 * (P.lt_max + 1);
     const int64_t S = P.cm.Npad;
-    int64_t *trow = im_tile + (int64_t)lane * O;
+    int64_t *trow = im_tile + (int64_t)(lane / LPE) * O;
 
     ImState<M1, BACKLOG> st;
     int t = t_u;
@@ -175,50 +218,64 @@ im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io) {
 #pragma unroll
         for (int i = 0; i < M1; i++) st.I[i] = P.I[i * S + e];
 #pragma unroll
-        for (int j = 0; j <= M1; j++) st.B[j] = BACKLOG ? P.B[j * S + e] : 0;
+        for (int q = 0; q <= M1; q++) st.B[q] = BACKLOG ? P.B[q * S + e] : 0;
         if (!TU) t = P.cm.period[e];
     }
     bool fault = false;
     for (int k = 0; k < io.K; k++) {
         const int64_t oi = (int64_t)k * N + e;
+        bool tr = false;
         if (valid) {
             if (t >= P.periods) {
                 if (P.cm.autoreset == AR_NEXT_STEP) {
-                    im_reset_regs<M1, BACKLOG>(P, st, trow);
-                    io.rew[oi] = 0.0;
-                    io.term[oi] = 0;
-                    io.trunc[oi] = 0;
+                    im_reset_regs<M1, BACKLOG>(P, st, trow, j);
+                    if (leader) {
+                        io.rew[oi] = 0.0;
+                        io.term[oi] = 0;
+                        io.trunc[oi] = 0;
+                    }
                     t = 0;
                 } else {
                     fault = true;  // stepping past the horizon (reference: IndexError)
                 }
             } else {
                 double r;
-                const bool tr = im_step_regs<M1, BACKLOG>(P, e, t, st, io.act + oi * M1, trow, r,
-                                                          k == io.K - 1 ? P.cm.info_demand : nullptr);
-                io.rew[oi] = r;
-                io.term[oi] = 0;
-                io.trunc[oi] = tr ? 1 : 0;
-                t += 1;
-                if (tr && P.cm.autoreset == AR_SAME_STEP) {
-                    if (io.fobs)
-                        for (int j = 0; j < O; j++) io.fobs[e * O + j] = trow[j];
-                    im_reset_regs<M1, BACKLOG>(P, st, trow);
-                    t = 0;
+                int64_t d;
+                tr = im_step_regs<M1, BACKLOG>(P, e, j, t, st, io.act + oi * M1, trow, r, d);
+                if (leader) {
+                    io.rew[oi] = r;
+                    io.term[oi] = 0;
+                    io.trunc[oi] = tr ? 1 : 0;
+                    if (k == io.K - 1 && P.cm.info_demand) P.cm.info_demand[e] = d;
                 }
+                t += 1;
             }
         }
         __syncthreads();
+        if (P.cm.autoreset == AR_SAME_STEP) {        // final obs out, then the reset obs in
+            if (valid && tr) {
+                if (io.fobs)
+                    for (int q = j; q < O; q += LPE) io.fobs[e * O + q] = trow[q];
+            }
+            __syncthreads();
+            if (valid && tr) {
+                im_reset_regs<M1, BACKLOG>(P, st, trow, j);
+                t = 0;
+            }
+            __syncthreads();
+        }
+#ifndef INVSIM_ABL_NO_OBS  // profiling ablation build only
         store_tile(im_tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+#endif
         __syncthreads();
     }
-    if (valid) {
+    if (valid && leader) {
         P.cm.rng.store_state(e, st.g);
 #pragma unroll
         for (int i = 0; i < M1; i++) P.I[i * S + e] = st.I[i];
         if (BACKLOG) {
 #pragma unroll
-            for (int j = 0; j <= M1; j++) P.B[j * S + e] = st.B[j];
+            for (int q = 0; q <= M1; q++) P.B[q * S + e] = st.B[q];
         }
         if (!TU) P.cm.period[e] = t;
         if (fault) atomicOr(P.cm.status, 1u);
@@ -232,15 +289,18 @@ im_reset_kernel(ImParams P, const uint8_t *__restrict__ mask, int64_t *__restric
     if (e >= P.cm.N) return;
     if (mask && !mask[e]) return;
     const int64_t S = P.cm.Npad;
-    ImState<M1, BACKLOG> st;
-    im_reset_regs<M1, BACKLOG>(P, st, obs ? obs + e * (M1 * (P.lt_max + 1)) : nullptr);
+    const int O = M1 * (P.lt_max + 1);
 #pragma unroll
-    for (int i = 0; i < M1; i++) P.I[i * S + e] = st.I[i];
+    for (int i = 0; i < M1; i++) P.I[i * S + e] = P.I0[i];
     if (BACKLOG) {
 #pragma unroll
-        for (int j = 0; j <= M1; j++) P.B[j * S + e] = 0;
+        for (int q = 0; q <= M1; q++) P.B[q * S + e] = 0;
     }
     P.cm.period[e] = 0;
+    if (obs) {
+        int64_t *orow = obs + e * O;
+        for (int q = 0; q < O; q++) orow[q] = (q < M1) ? P.I0[q] : 0;
+    }
 }
 
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -263,9 +323,8 @@ inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / b
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u,
                          const StepIO<int64_t, int64_t> &io, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
-    const size_t lds = (size_t)WAVE * M1 * (p.lt_max + 1) * sizeof(int64_t);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;  // host validates obs_dim <= 320
-    const dim3 grid(grid_for(p.cm.N, WAVE)), block(WAVE);
+    const size_t lds = (size_t)EPW * M1 * (p.lt_max + 1) * sizeof(int64_t);
+    const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
 #define L_(M, B)                                                                              \
     do {                                                                                      \
         if (t_u >= 0)                                                                         \

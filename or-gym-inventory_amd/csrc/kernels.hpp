@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #include "device_common.hpp"
+#include "group_rng.hpp"
 
 namespace invsim {
 
@@ -47,6 +48,7 @@ struct ImParams {
     int64_t I0[IM_MAX_M1];
     double up[IM_MAX_M1 + 1], uc[IM_MAX_M1 + 1], hc[IM_MAX_M1 + 1], kc[IM_MAX_M1 + 1];
     PtrsConst pc;                // Poisson(mu) constants, host libm
+    const double *rhs;           // PTRS right-hand-side table (host libm), pc.k0 .. pc.k0+pc.nk
     const double *alpha_pow;     // [periods]  alpha ** t (Python float pow)
     const int64_t *user_D;       // [periods]
     int64_t *I;                  // [M1][Npad]   on-hand inventory I[t]
@@ -63,10 +65,12 @@ struct NetParams {
     const double *I0, *h, *C, *o, *v;
     const int32_t *is_factory, *is_retail;
     const int32_t *sup, *pur, *sup_is_factory, *L, *ring_off;
+    const int32_t *win_off;      // [E] obs offset of link e's order window (links with L > 0)
     const double *lp, *lg;
     const int32_t *rl_node, *rl_user;
     const double *rl_p, *rl_b;
     const PtrsConst *rl_pc;      // [RL]
+    const double *rhs;           // PTRS right-hand-side tables of all retail links (rl_pc[r].toff)
     const double *user_D;        // [RL][T]
     const int32_t *succ_ptr, *succ_kind, *succ_idx, *pred_ptr, *pred_idx;
     const double *alpha_pow;     // [T]
@@ -101,7 +105,22 @@ __host__ __device__ inline int next_period(int t, int horizon, int autoreset, bo
     return t1;
 }
 
-constexpr int WAVE = 64;  // one-wave workgroups: LDS obs tile stored with 16-B coalesced rows
+constexpr int WAVE = 64;          // one-wave workgroups: LDS obs tile stored with 16-B coalesced rows
+// Lanes per env.  1 = one thread per env with the sequential sampler; GRP (4) =
+// the lane-group sampler of group_rng.hpp.  tools/poisson_bench.hip measured the
+// sequential sampler (host RHS table + f32 pre-test) 1.1-1.6x faster than the
+// group one at 65 536 - 524 288 envs on MI355X, so 1 it is.
+constexpr int LPE = 1;
+constexpr int EPW = WAVE / LPE;   // envs per wave
+
+__device__ __forceinline__ int64_t env_poisson(Pcg &g, const PtrsConst &c, const double *rhs) {
+    if (LPE == 1) return np_poisson(g, c, rhs);
+    return np_poisson_grp(g, c, rhs);
+}
+__device__ __forceinline__ int64_t env_poisson_dyn(Pcg &g, double lam) {
+    if (LPE == 1) return np_poisson_dyn(g, lam);
+    return np_poisson_dyn_grp(g, lam);
+}
 
 // Copy `count` elements of an LDS tile to global memory, 16 B per lane.
 template <typename T>

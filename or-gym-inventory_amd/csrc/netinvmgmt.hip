@@ -54,10 +54,14 @@ __device__ __forceinline__ void net_reset_lds(const NetParams &P, NetScratch &s,
 }
 
 // One step (:436-635) at period t < T.  Returns truncated.
-__device__ bool net_step_lds(const NetParams &P, int64_t e, int t, Pcg &g, NetScratch &s,
+// All LPE lanes of the env run it (redundant node/link arithmetic in private
+// LDS scratch, lane-group Poisson draws); lane j == 0 writes state and the
+// U/X part of the obs row, lane j writes the order windows of links k = j mod LPE.
+__device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, Pcg &g, NetScratch &s,
                              const float *__restrict__ arow, float *orow, double &reward, int64_t *dem) {
     const int64_t S = P.cm.Npad;
     const int J = P.J, E = P.E, RL = P.RL;
+    const bool leader = gl == 0;
     // market demand draws first (retail-link order, :536-541): RNG-only work
     for (int r = 0; r < RL; r++) {
         double dd;
@@ -66,11 +70,12 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int t, Pcg &g, NetSc
             dd = rint(P.user_D[(int64_t)r * P.T + idx]);       // max(0, int(round(x)))
             if (!(dd > 0)) dd = 0.0;
         } else {
-            const int64_t pd = np_poisson(g, P.rl_pc[r]);
+            const PtrsConst &pc = P.rl_pc[r];
+            const int64_t pd = env_poisson(g, pc, P.rhs ? P.rhs + pc.toff : nullptr);
             dd = (double)(pd > 0 ? pd : 0);
         }
         LV(s.Dd, r) = dd;
-        if (dem) dem[e * RL + r] = (int64_t)dd;
+        if (dem && leader) dem[e * RL + r] = (int64_t)dd;
     }
     for (int j = 0; j < J; j++) {
         LV(s.cons, j) = 0.0;
@@ -106,7 +111,7 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int t, Pcg &g, NetSc
         } else {
             const int64_t row = P.ring_off[k] + (int)((uint32_t)t % (uint32_t)L);
             if (t >= L) a = P.Rring[row * S + e];
-            P.Rring[row * S + e] = LV(s.Rn, k);
+            if (leader) P.Rring[row * S + e] = LV(s.Rn, k);
         }
         LV(s.arrv, k) = a;
         LV(s.Y, k) = LV(s.Y, k) - a + LV(s.Rn, k);
@@ -156,12 +161,15 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int t, Pcg &g, NetSc
     // obs (:334-413): U[t+1] (RL), X[t+1] (J), then for each link with L>0 in
     // sorted order the fulfilled orders R[t+1-L .. t] right-aligned, zero before t=0
     if (orow) {
-        int o = 0;
-        for (int r = 0; r < RL; r++) orow[o++] = (float)LV(s.U, r);
-        for (int j = 0; j < J; j++) orow[o++] = (float)LV(s.X, j);
-        for (int k = 0; k < E; k++) {
+        if (leader) {
+            int o = 0;
+            for (int r = 0; r < RL; r++) orow[o++] = (float)LV(s.U, r);
+            for (int q = 0; q < J; q++) orow[o++] = (float)LV(s.X, q);
+        }
+        for (int k = gl; k < E; k += LPE) {
             const int L = P.L[k];
             if (L == 0) continue;
+            float *w = orow + P.win_off[k];
             for (int p = 0; p < L - 1; p++) {
                 const int age = L - 1 - p;                  // R[t - age]
                 double v = 0.0;
@@ -169,9 +177,9 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int t, Pcg &g, NetSc
                     const int64_t row = P.ring_off[k] + (int)((uint32_t)(t - age) % (uint32_t)L);
                     v = P.Rring[row * S + e];
                 }
-                orow[o++] = (float)v;
+                w[p] = (float)v;
             }
-            orow[o++] = (float)LV(s.Rn, k);
+            w[L - 1] = (float)LV(s.Rn, k);
         }
     }
     return t + 1 >= P.T;
@@ -182,17 +190,19 @@ __global__ void __launch_bounds__(WAVE)
 net_run_kernel(NetParams P, int t_u, StepIO<float, float> io) {
     extern __shared__ __attribute__((aligned(16))) double net_lds[];
     const int lane = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
-    const int64_t e = e0 + lane;
+    const int gl = lane & (LPE - 1);
+    const bool leader = gl == 0;
+    const int64_t e0 = (int64_t)blockIdx.x * EPW;
+    const int64_t e = e0 + lane / LPE;
     const int64_t N = P.cm.N;
     const bool valid = e < N;
-    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
+    const int nvalid = (int)((N - e0) < EPW ? (N - e0) : EPW);
     const int O = P.RL + P.J + P.sumL;
     const int64_t S = P.cm.Npad;
     const int rows = scratch_rows(P.J, P.E, P.RL);
-    NetScratch s = scratch_of(P, net_lds + lane);
+    NetScratch s = scratch_of(P, net_lds + lane);   // private scratch per lane
     float *tile = reinterpret_cast<float *>(net_lds + (int64_t)rows * WAVE);
-    float *trow = tile + (int64_t)lane * O;
+    float *trow = tile + (int64_t)(lane / LPE) * O;
 
     Pcg g;
     int t = t_u;
@@ -206,38 +216,47 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io) {
     bool fault = false;
     for (int k = 0; k < io.K; k++) {
         const int64_t oi = (int64_t)k * N + e;
+        bool tr = false;
         if (valid) {
             if (t >= P.T) {
                 if (P.cm.autoreset == AR_NEXT_STEP) {
-                    net_reset_lds(P, s, trow);
-                    io.rew[oi] = 0.0;
-                    io.term[oi] = 0;
-                    io.trunc[oi] = 0;
+                    net_reset_lds(P, s, leader ? trow : nullptr);
+                    if (leader) {
+                        io.rew[oi] = 0.0;
+                        io.term[oi] = 0;
+                        io.trunc[oi] = 0;
+                    }
                     t = 0;
                 } else {
                     fault = true;
                 }
             } else {
                 double r;
-                const bool tr = net_step_lds(P, e, t, g, s, io.act + oi * P.E, trow, r,
-                                             k == io.K - 1 ? P.cm.info_demand : nullptr);
-                io.rew[oi] = r;
-                io.term[oi] = 0;
-                io.trunc[oi] = tr ? 1 : 0;
-                t += 1;
-                if (tr && P.cm.autoreset == AR_SAME_STEP) {
-                    if (io.fobs)
-                        for (int j = 0; j < O; j++) io.fobs[e * O + j] = trow[j];
-                    net_reset_lds(P, s, trow);
-                    t = 0;
+                tr = net_step_lds(P, e, gl, t, g, s, io.act + oi * P.E, trow, r,
+                                  k == io.K - 1 ? P.cm.info_demand : nullptr);
+                if (leader) {
+                    io.rew[oi] = r;
+                    io.term[oi] = 0;
+                    io.trunc[oi] = tr ? 1 : 0;
                 }
+                t += 1;
             }
         }
         __syncthreads();
+        if (P.cm.autoreset == AR_SAME_STEP) {        // final obs out, then the reset obs in
+            if (valid && tr && io.fobs)
+                for (int q = gl; q < O; q += LPE) io.fobs[e * O + q] = trow[q];
+            __syncthreads();
+            if (valid && tr) {
+                net_reset_lds(P, s, leader ? trow : nullptr);
+                t = 0;
+            }
+            __syncthreads();
+        }
         store_tile(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
         __syncthreads();
     }
-    if (valid) {
+    if (valid && leader) {
         P.cm.rng.store_state(e, g);
         for (int j = 0; j < P.J; j++) P.X[j * S + e] = LV(s.X, j);
         for (int r = 0; r < P.RL; r++) P.U[r * S + e] = LV(s.U, r);
@@ -273,7 +292,7 @@ inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / b
 }  // namespace
 
 size_t net_lds_bytes(const NetParams &p) {
-    const size_t tile = (size_t)WAVE * (p.RL + p.J + p.sumL) * sizeof(float);
+    const size_t tile = (size_t)EPW * (p.RL + p.J + p.sumL) * sizeof(float);
     return (size_t)scratch_rows(p.J, p.E, p.RL) * WAVE * sizeof(double) + (tile + 15) / 16 * 16;
 }
 
@@ -281,7 +300,7 @@ hipError_t net_run_launch(const NetParams &p, int t_u, const StepIO<float, float
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = net_lds_bytes(p);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    const dim3 grid(grid_for(p.cm.N, WAVE)), block(WAVE);
+    const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
     if (t_u >= 0)
         hipLaunchKernelGGL(net_run_kernel<true>, grid, block, lds, s, p, t_u, io);
     else

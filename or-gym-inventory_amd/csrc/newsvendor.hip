@@ -1,5 +1,5 @@
 // NewsvendorEnv.step / reset (newsvendor.py:100-204) as HIP kernels for
-// gfx950: one thread per env, one wave per workgroup, K steps per launch.
+// gfx950: one wave = 16 envs x 4 lanes (group_rng.hpp), K steps per launch.
 //
 // Per-env HBM state (SoA rows of Npad): params price,cost,h,k,mu (f64: they
 // are Python floats in the reference), the order pipeline as a ring of L f32
@@ -61,7 +61,8 @@ __device__ __forceinline__ void obs_params(const double *par, float *orow) {
 
 // newsvendor.py:100-123: 5 uniforms, params, empty pipeline, obs row
 template <int LT>
-__device__ __forceinline__ void nv_reset_regs(const NvParams &P, int64_t e, NvState<LT> &s, float *orow) {
+__device__ __forceinline__ void nv_reset_regs(const NvParams &P, int64_t e, NvState<LT> &s, float *orow,
+                                              bool leader) {
     double price = s.g.next_double() * P.p_max;
     if (!(price > 1)) price = 1;                        // max(1, x)
     double cost = s.g.next_double() * price;
@@ -72,8 +73,8 @@ __device__ __forceinline__ void nv_reset_regs(const NvParams &P, int64_t e, NvSt
     const double mu = s.g.next_double() * P.mu_max;
     s.par[0] = price; s.par[1] = cost; s.par[2] = hh; s.par[3] = kk; s.par[4] = mu;
     const int64_t S = P.cm.Npad;
-#pragma unroll
-    for (int j = 0; j < 5; j++) P.par[j * S + e] = s.par[j];
+    if (leader)
+        for (int j = 0; j < 5; j++) P.par[j * S + e] = s.par[j];
     if (LT > 0) {
 #pragma unroll
         for (int p = 0; p < (LT > 0 ? LT : 1); p++) s.pv[p] = 0.f;
@@ -97,7 +98,7 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, int s
         sl = sl >= L ? sl - L : sl;
         return (p >= L - sc) ? P.pipe[(int64_t)sl * S + e] : 0.f;
     };
-    const int64_t d = np_poisson_dyn(s.g, s.par[4]);                       // :146
+    const int64_t d = env_poisson_dyn(s.g, s.par[4]);                      // :146
     const Tv ZERO = tv(0.0, K_PY);
     const Tv oq = tv(np_clip((double)action, 0.0, P.max_order), K_F64);    // :131-132
     const float S5 = np_sum<float>(L, pos);                                 // :135
@@ -122,7 +123,7 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, int s
         for (int p = 0; p + 1 < L; p++) orow[5 + p] = pos(p + 1);
         if (L > 0) orow[5 + L - 1] = qf;
     }
-    if (L > 0) P.pipe[(int64_t)base * S + e] = qf;                         // replaces the arrived slot
+    if (L > 0 && orow) P.pipe[(int64_t)base * S + e] = qf;                 // leader: replaces the arrived slot
     if (LT > 0) {
 #pragma unroll
         for (int p = 0; p + 1 < (LT > 0 ? LT : 1); p++) s.pv[p] = s.pv[p + 1];
@@ -138,14 +139,15 @@ __global__ void __launch_bounds__(WAVE)
 nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
     extern __shared__ __attribute__((aligned(16))) float nv_tile[];
     const int lane = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
-    const int64_t e = e0 + lane;
+    const bool leader = (lane & (LPE - 1)) == 0;
+    const int64_t e0 = (int64_t)blockIdx.x * EPW;
+    const int64_t e = e0 + lane / LPE;
     const int64_t N = P.cm.N;
     const bool valid = e < N;
-    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
+    const int nvalid = (int)((N - e0) < EPW ? (N - e0) : EPW);
     const int O = P.L + 5;
     const int64_t S = P.cm.Npad;
-    float *trow = nv_tile + (int64_t)lane * O;
+    float *trow = leader ? nv_tile + (int64_t)(lane / LPE) * O : nullptr;  // leader writes obs/state
 
     NvState<LT> st;
     int sc = t_u;
@@ -168,23 +170,27 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
         const int64_t oi = (int64_t)k * N + e;
         if (valid) {
             if (P.cm.autoreset == AR_NEXT_STEP && sc >= P.step_limit) {
-                nv_reset_regs<LT>(P, e, st, trow);
-                io.rew[oi] = 0.0;
-                io.term[oi] = 0;
-                io.trunc[oi] = 0;
+                nv_reset_regs<LT>(P, e, st, trow, leader);
+                if (leader) {
+                    io.rew[oi] = 0.0;
+                    io.term[oi] = 0;
+                    io.trunc[oi] = 0;
+                }
                 sc = 0;
             } else {
                 double r;
                 const bool tr = nv_step_regs<LT>(P, e, sc, st, io.act[oi], trow, r,
-                                                 k == io.K - 1 ? P.cm.info_demand : nullptr);
-                io.rew[oi] = r;
-                io.term[oi] = 0;
-                io.trunc[oi] = tr ? 1 : 0;
+                                                 (leader && k == io.K - 1) ? P.cm.info_demand : nullptr);
+                if (leader) {
+                    io.rew[oi] = r;
+                    io.term[oi] = 0;
+                    io.trunc[oi] = tr ? 1 : 0;
+                }
                 sc += 1;
                 if (tr && P.cm.autoreset == AR_SAME_STEP) {
-                    if (io.fobs)
+                    if (io.fobs && leader)
                         for (int j = 0; j < O; j++) io.fobs[e * O + j] = trow[j];
-                    nv_reset_regs<LT>(P, e, st, trow);
+                    nv_reset_regs<LT>(P, e, st, trow, leader);
                     sc = 0;
                 }
             }
@@ -193,7 +199,7 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
         store_tile(nv_tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
         __syncthreads();
     }
-    if (valid) {
+    if (valid && leader) {
         P.cm.rng.store_state(e, st.g);
         if (!TU) P.cm.period[e] = sc;
     }
@@ -206,7 +212,7 @@ nv_reset_kernel(NvParams P, const uint8_t *__restrict__ mask, float *__restrict_
     if (mask && !mask[e]) return;
     NvState<-1> st;
     st.g = P.cm.rng.load(e);
-    nv_reset_regs<-1>(P, e, st, obs ? obs + e * (P.L + 5) : nullptr);
+    nv_reset_regs<-1>(P, e, st, obs ? obs + e * (P.L + 5) : nullptr, true);
     P.cm.rng.store_state(e, st.g);
     P.cm.period[e] = 0;
 }
@@ -217,8 +223,8 @@ inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / b
 
 hipError_t nv_run_launch(const NvParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
-    const size_t lds = (size_t)WAVE * (p.L + 5) * sizeof(float);
-    const dim3 grid(grid_for(p.cm.N, WAVE)), block(WAVE);
+    const size_t lds = (size_t)EPW * (p.L + 5) * sizeof(float);
+    const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
 #define L_(X)                                                                                 \
     do {                                                                                      \
         if (t_u >= 0)                                                                         \

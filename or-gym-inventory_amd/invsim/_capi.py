@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libinvsim.so")
+# INVSIM_LIB: load another build of the same ABI (profiling ablations, tools/)
+LIB_PATH = os.environ.get("INVSIM_LIB") or os.path.join(HERE, "_lib", "libinvsim.so")
 CSRC = os.path.normpath(os.path.join(HERE, "..", "csrc"))
 
 INVSIM_NEWSVENDOR, INVSIM_INVMGMT, INVSIM_NETINVMGMT = 1, 2, 3

@@ -44,7 +44,11 @@ def drive_golden(env, fx, cfg, demand_key="demand"):
             s = ep * L + k
             a = torch.from_numpy(np.ascontiguousarray(fx["actions"][:, s])).to(env.device)
             o, r, te, tr, info = env.step(a)
-            assert _eq_bits(o.cpu().numpy(), fx["obs"][:, s]), f"obs mismatch step {s}"
+            on = o.cpu().numpy()
+            if not _eq_bits(on, fx["obs"][:, s]):
+                bad = np.argwhere(on != fx["obs"][:, s])[:4]
+                pytest.fail(f"obs mismatch step {s} at {bad.tolist()}: got {[on[tuple(b)] for b in bad]}, "
+                            f"expected {[fx['obs'][:, s][tuple(b)] for b in bad]}, actions {fx['actions'][bad[0][0], max(0, s-2):s+1].tolist()}")
             _assert_reward(r.cpu().numpy(), fx["reward"][:, s], f"step {s}")
             assert not te.any()
             assert np.array_equal(tr.cpu().numpy(), fx["truncated"][:, s]), f"truncated step {s}"
