@@ -175,9 +175,16 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    # HIP events on the stream the kernels run on, around the timed region:
+    # launches are back to back there, so (end - start) / calls is the mean
+    # kernel duration (+ inter-kernel gaps, ~0 on a saturated queue)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(calls):
         one(i)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -188,17 +195,7 @@ def main():
         el = float(t.item())
     total_steps = calls * steps_per_call  # env.step() calls over the batch
     env_steps = total_steps * N * world
-
-    # kernel-only duration via HIP events on the kernel's stream (per launch)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(min(calls, 200))]
-    for i, (a, b) in enumerate(ev):
-        a.record(stream)
-        one(i)
-        b.record(stream)
-    torch.cuda.synchronize(dev)
-    kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
-    kern_ms_mean = sum(kern_ms) / len(kern_ms)
+    kern_ms_mean = ev0.elapsed_time(ev1) / calls
 
     # episodic-return statistics all-reduced across GPUs (RCCL): one short episode
     env2 = getattr(invsim, wl["cls"])(min(N, 4096), device=dev, global_offset=rank * N)
@@ -218,6 +215,11 @@ def main():
 
     B = wl["B_io"] + (wl["B_state_rollout"] / K if K else wl["B_state"])
     achieved = B * N * steps_per_call / (kern_ms_mean * 1e-3) / 1e9
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "r01", f"pmc_{args.workload}.json")
+    if os.path.exists(pmc) and args.mode == "step" and N == wl["n"]:
+        rec = json.load(open(pmc))
+        traffic, traffic_src = rec["hbm_bytes_per_launch"], os.path.relpath(pmc, ROOT)
     out = {
         "metric": "env-steps/sec (batched) at 1/2/4/8 MI355X; % HBM roofline",
         "value": env_steps / el,
@@ -235,9 +237,12 @@ def main():
                    "mode": args.mode + (f" K={K}" if K else ""), "autoreset": "next_step",
                    "parallelism": f"dp{world} (env sharding, no data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, calibrated)",
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": B * N * steps_per_call,
                      "bytes_per_env_step": B, "kernel_ms_mean": kern_ms_mean,
-                     "kernel_ms_median": kern_ms[len(kern_ms) // 2]},
+                     "kernel_timing": "HIP events on the kernel stream around the timed region / launches"},
         "episode_stats": {"sum_return": stats[0], "sum_sq_return": stats[1], "episodes": stats[2]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
