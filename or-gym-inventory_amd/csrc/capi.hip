@@ -185,9 +185,13 @@ void rhs_table(PtrsConst &c, std::vector<double> &tab) {
     c.toff = (int32_t)tab.size();
     if (!(c.lam >= 10) || c.lam > 1e8) return;
     const double sd = std::sqrt(c.lam);
-    const int64_t k0 = std::max<int64_t>(0, (int64_t)std::floor(c.lam - 12 * sd - 10));
+    int64_t k0 = std::max<int64_t>(0, (int64_t)std::floor(c.lam - 12 * sd - 10));
     const int64_t k1 = (int64_t)std::ceil(c.lam + 12 * sd + 40);
-    const int64_t n = std::min<int64_t>(k1 - k0, 16384);
+    int64_t n = k1 - k0;
+    if (n > RHS_LDS_MAX) {      // keep the central RHS_LDS_MAX entries (the rest: device)
+        k0 = std::max<int64_t>(0, (int64_t)std::floor(c.lam) - RHS_LDS_MAX / 2 + 20);
+        n = RHS_LDS_MAX;
+    }
     for (int64_t k = k0; k < k0 + n; k++)
         tab.push_back(-c.lam + (double)k * c.loglam - np_loggam((double)(k + 1)));
     c.k0 = (int32_t)k0;

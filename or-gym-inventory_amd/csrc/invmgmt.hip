@@ -27,7 +27,13 @@
 namespace invsim {
 namespace {
 
-constexpr int IM_WLANE = (36 + LPE - 1) / LPE;  // obs-window entries per lane kept in registers (27 needed at D=10, M1=3)
+#ifdef INVSIM_TIMING
+__device__ uint64_t g_tbuf[TB_WAVES * TB_PROBES];
+#endif
+
+// obs-window entries per lane kept in registers: the (lt_max - 1) * M1 entries
+// of lt_max <= 10, capped at 36 (longer windows are copied ring -> LDS directly)
+constexpr int im_wlane(int m1) { return (9 * m1 < 36 ? 9 * m1 : 36 + LPE - 1) / LPE; }
 
 // numpy int64 array arithmetic wraps around (two's complement)
 __device__ __forceinline__ int64_t wrap_add(int64_t a, int64_t b) {
@@ -42,6 +48,20 @@ __device__ __forceinline__ int64_t min_via_f64(int64_t a, int64_t sup) {
     const double x = (double)a, y = (double)sup;
     return (int64_t)((x <= y) ? x : y);
 }
+
+// PTRS RHS table values loaded by each lane, written to the LDS table once the
+// step's global loads are all in flight (a wait for these loads would
+// otherwise hold back every load issued after it)
+struct TableStage {
+    static constexpr int NT = RHS_LDS_MAX / WAVE;
+    double *dst;
+    double v[NT];
+    __device__ __forceinline__ void flush(int lane) {
+#pragma unroll
+        for (int u = 0; u < NT; u++) dst[lane + u * WAVE] = v[u];
+        __builtin_amdgcn_wave_barrier();
+    }
+};
 
 template <int M1, bool BACKLOG>
 struct ImState {
@@ -67,13 +87,14 @@ __device__ __forceinline__ void im_reset_regs(const ImParams &P, ImState<M1, BAC
 
 // One step (:224-352) at period t < periods.  Returns truncated.
 template <int M1, bool BACKLOG>
-__device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int j, int t,
+__device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool valid, int j, int t,
                                              ImState<M1, BACKLOG> &s,
                                              const int64_t *__restrict__ arow, int64_t *orow,
+                                             const double *rhs, TableStage *ts, double apow, int64_t udem,
                                              double &reward, int64_t &dem_out) {
     const int64_t S = P.cm.Npad;
     const int D = P.lt_max;
-    const bool leader = j == 0;
+    const bool leader = valid && j == 0;   // state writes
     // Phase A: every load of the step up front (actions, arrivals, this lane's
     // share of the observation window) so the latency overlaps the demand draw
     int64_t req[M1], ordreq[M1], R[M1], arr[M1];
@@ -81,10 +102,12 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int j
     for (int i = 0; i < M1; i++) req[i] = arow[i];
 #pragma unroll
     for (int i = 0; i < M1; i++) {                                  // arrivals R[t-L_i] (:271-277)
+        // unconditional load (row 0 when L = 0: the ring always has a row) so the
+        // step's loads are straight-line and their waits exact; masked below
         const int L = P.L[i];
-        arr[i] = 0;
-        if (L > 0 && t >= L)
-            arr[i] = P.Rring[(int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e];
+        const int row = L > 0 ? P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L) : 0;
+        arr[i] = P.Rring[(int64_t)row * S + e];
+        if (!(L > 0 && t >= L)) arr[i] = 0;
     }
     // window rows t+1-n .. t-1 of the action_log ring (:380): nw entries, lane j
     // takes entries q = j, j+4, ...
@@ -98,24 +121,31 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int j
         slot = slot >= D ? slot - D : slot;
         return P.alog + ((int64_t)slot * M1 + i) * S + e;
     };
-    const bool wreg = orow && nw <= IM_WLANE * LPE;
-    int64_t wv[IM_WLANE];
+    constexpr int WL = im_wlane(M1);
+    const bool wreg = orow && (D - 1) * M1 <= WL * LPE;   // launch-uniform
+    int64_t wv[WL];
 #ifndef INVSIM_ABL_NO_WINDOW
-    if (wreg) {
+    {   // unconditional (straight-line loads, exact vmcnt waits): entries past nw
+        // (start of an episode) re-read the last valid one, or entry 0, always a
+        // valid ring row; unused when !wreg
+        const int qmax = nw > 0 ? nw - 1 : 0;
 #pragma unroll
-        for (int u = 0; u < IM_WLANE; u++) {
+        for (int u = 0; u < WL; u++) {
             const int q = j + u * LPE;
-            wv[u] = (q < nw) ? *wsrc(q) : 0;
+            wv[u] = *wsrc(q < qmax ? q : qmax);
         }
     }
 #endif
+    TPROBE(1);   // step loads issued
+    if (ts) ts->flush((int)threadIdx.x);
     // Phase B: demand, a function of the RNG stream only (:172, :280)
 #ifdef INVSIM_ABL_NO_POISSON  // profiling ablation build only (wrong results)
     int64_t d = 20 + (int64_t)(s.g.lo & 3);
 #else
-    int64_t d = (P.dist == 5) ? P.user_D[t] : env_poisson(s.g, P.pc, P.rhs);
+    int64_t d = (P.dist == 5) ? udem : env_poisson(s.g, P.pc, rhs);
 #endif
     if (d < 0) d = 0;
+    TPROBE(2);
     // Phase C: dynamics (identical in the 4 lanes)
 #pragma unroll
     for (int i = 0; i < M1; i++) req[i] = req[i] > 0 ? req[i] : 0;  // :250
@@ -133,7 +163,7 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int j
         const int L = P.L[i];
         Icur[i] = wrap_add(s.I[i], L == 0 ? R[i] : arr[i]);
         if (L > 0 && leader)
-            P.Rring[(int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e] = R[i];
+            st_store(P.Rring + (int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e, R[i]);
     }
     const int64_t dfill = wrap_add(d, s.B[0]);                      // :284-286
     const int64_t s0 = Icur[0] < dfill ? Icur[0] : dfill;           // :288
@@ -156,7 +186,7 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int j
         term[q] = ((P.up[q] * Sj - P.uc[q] * Sj) - hold) - P.kc[q] * (double)U[q];
     }
     const double profit = np_sum<double>(M1 + 1, [&](int q) { return term[q]; });
-    reward = P.alpha_pow[t] * profit;                               // :322
+    reward = apow * profit;                                         // :322
 #pragma unroll
     for (int i = 0; i < M1; i++) s.I[i] = Icur[i];                  // :326
 #pragma unroll
@@ -164,7 +194,7 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int j
     dem_out = d;
     if (orow) {                                                     // :354-391
         int64_t *w = orow + M1;
-        if (leader) {
+        if (j == 0) {
 #pragma unroll
             for (int i = 0; i < M1; i++) orow[i] = Icur[i];
             if (D > 0) {
@@ -175,7 +205,7 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int j
         if (D > 0) {
             if (wreg) {
 #pragma unroll
-                for (int u = 0; u < IM_WLANE; u++) {
+                for (int u = 0; u < WL; u++) {
                     const int q = j + u * LPE;
                     if (q < nw) w[q] = wv[u];
                 }
@@ -190,12 +220,78 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, int j
     if (D > 0 && leader) {
         const int wslot = (int)((uint32_t)t % (uint32_t)D);
 #pragma unroll
-        for (int i = 0; i < M1; i++) P.alog[((int64_t)wslot * M1 + i) * S + e] = req[i];  // :268
+        for (int i = 0; i < M1; i++) st_store(P.alog + ((int64_t)wslot * M1 + i) * S + e, req[i]);  // :268
     }
+    TPROBE(3);
     return t1 >= P.periods;                                         // :350
 }
 
-template <int M1, bool BACKLOG, bool TU>
+// Step k of a launch for the wave's envs: step (or NEXT_STEP reset) into the
+// LDS obs tile, SAME_STEP final-obs/reset, then the tile's coalesced store.
+template <int M1, bool BACKLOG, bool STEP_ONLY>
+__device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<int64_t, int64_t> &io, int k,
+                                               int64_t e, int64_t e0, int lane, bool valid, int nvalid,
+                                               ImState<M1, BACKLOG> &st, int &t, bool &fault,
+                                               int64_t *tile, int64_t *trow, const double *rhs,
+                                               TableStage *ts, const double *pre_apow, const int64_t *pre_udem) {
+    const int j = lane & (LPE - 1);
+    const bool leader = j == 0;
+    const int64_t N = P.cm.N;
+    const int O = M1 * (P.lt_max + 1);
+    const int64_t oi = (int64_t)k * N + e;
+    bool tr = false;
+    if (!STEP_ONLY && t >= P.periods) {
+        if (P.cm.autoreset == AR_NEXT_STEP) {
+            im_reset_regs<M1, BACKLOG>(P, st, trow, j);
+            if (valid && leader) {
+                out_store(io.rew + oi, 0.0);
+                out_store(io.term + oi, (uint8_t)0);
+                out_store(io.trunc + oi, (uint8_t)0);
+            }
+            t = 0;
+        } else {
+            fault = true;  // stepping past the horizon (reference: IndexError)
+        }
+    } else {
+        // every lane steps (lanes past N read padded state columns and the last
+        // env's actions); only valid lanes store
+        double r;
+        int64_t d;
+        const int64_t ea = valid ? oi : (int64_t)k * N + (N - 1);
+        // per-period scalars (alpha**t, user_D[t]: always a valid table), loaded
+        // before any store of the step (vmcnt counts stores too) unless preloaded
+        const double apow = pre_apow ? *pre_apow : P.alpha_pow[t];
+        const int64_t udem = pre_udem ? *pre_udem : P.user_D[t];
+        tr = im_step_regs<M1, BACKLOG>(P, e, valid, j, t, st, io.act + ea * M1, trow, rhs, ts, apow, udem, r, d);
+        if (valid && leader) {
+            out_store(io.rew + oi, r);
+            out_store(io.term + oi, (uint8_t)0);
+            out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
+            if (k == io.K - 1 && P.cm.info_demand) P.cm.info_demand[e] = d;
+        }
+        t += 1;
+    }
+    wave_lds_sync();
+    if (P.cm.autoreset == AR_SAME_STEP) {        // final obs out, then the reset obs in
+        if (valid && tr && io.fobs)
+            for (int q = j; q < O; q += LPE) io.fobs[e * O + q] = trow[q];
+        wave_lds_sync();
+        if (tr) {
+            im_reset_regs<M1, BACKLOG>(P, st, trow, j);
+            t = 0;
+        }
+        wave_lds_sync();
+    }
+#ifndef INVSIM_ABL_NO_OBS  // profiling ablation build only
+    // obs tile: at most 64 * M1 * 11 int64 in register-window configurations
+    store_tile<(M1 * 11 * EPW * 8 + 16 * WAVE - 1) / (16 * WAVE)>(tile, io.obs + ((int64_t)k * N + e0) * O,
+                                                                 (int64_t)nvalid * O, lane);
+#endif
+    TPROBE(4);
+    wave_lds_sync();
+}
+
+template <int M1, bool BACKLOG, bool TU, bool ONE>
 __global__ void __launch_bounds__(WAVE)
 im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io) {
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
@@ -210,76 +306,81 @@ im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io) {
     const int O = M1 * (P.lt_max + 1);
     const int64_t S = P.cm.Npad;
     int64_t *trow = im_tile + (int64_t)(lane / LPE) * O;
-
-    ImState<M1, BACKLOG> st;
-    int t = t_u;
-    if (valid) {
-        st.g = P.cm.rng.load(e);
-#pragma unroll
-        for (int i = 0; i < M1; i++) st.I[i] = P.I[i * S + e];
-#pragma unroll
-        for (int q = 0; q <= M1; q++) st.B[q] = BACKLOG ? P.B[q * S + e] : 0;
-        if (!TU) t = P.cm.period[e];
-    }
-    bool fault = false;
-    for (int k = 0; k < io.K; k++) {
-        const int64_t oi = (int64_t)k * N + e;
-        bool tr = false;
+    TPROBE(0);
+    TPROBE_ID();
+    if (ONE && TU && t_u >= P.periods) {
+        // lock-step NEXT_STEP autoreset of the whole batch (the host refuses a
+        // DISABLED overrun when the period is lock-step, and SAME_STEP resets in
+        // the done step): no state to load, so a separate straight path
         if (valid) {
-            if (t >= P.periods) {
-                if (P.cm.autoreset == AR_NEXT_STEP) {
-                    im_reset_regs<M1, BACKLOG>(P, st, trow, j);
-                    if (leader) {
-                        io.rew[oi] = 0.0;
-                        io.term[oi] = 0;
-                        io.trunc[oi] = 0;
-                    }
-                    t = 0;
-                } else {
-                    fault = true;  // stepping past the horizon (reference: IndexError)
-                }
-            } else {
-                double r;
-                int64_t d;
-                tr = im_step_regs<M1, BACKLOG>(P, e, j, t, st, io.act + oi * M1, trow, r, d);
-                if (leader) {
-                    io.rew[oi] = r;
-                    io.term[oi] = 0;
-                    io.trunc[oi] = tr ? 1 : 0;
-                    if (k == io.K - 1 && P.cm.info_demand) P.cm.info_demand[e] = d;
-                }
-                t += 1;
+#pragma unroll
+            for (int i = 0; i < M1; i++) P.I[i * S + e] = P.I0[i];
+            if (BACKLOG) {
+#pragma unroll
+                for (int q = 0; q <= M1; q++) P.B[q * S + e] = 0;
             }
+            out_store(io.rew + e, 0.0);
+            out_store(io.term + e, (uint8_t)0);
+            out_store(io.trunc + e, (uint8_t)0);
         }
-        __syncthreads();
-        if (P.cm.autoreset == AR_SAME_STEP) {        // final obs out, then the reset obs in
-            if (valid && tr) {
-                if (io.fobs)
-                    for (int q = j; q < O; q += LPE) io.fobs[e * O + q] = trow[q];
-            }
-            __syncthreads();
-            if (valid && tr) {
-                im_reset_regs<M1, BACKLOG>(P, st, trow, j);
-                t = 0;
-            }
-            __syncthreads();
-        }
-#ifndef INVSIM_ABL_NO_OBS  // profiling ablation build only
-        store_tile(im_tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
-#endif
-        __syncthreads();
+        for (int q = 0; q < O; q++) trow[q] = (q < M1) ? P.I0[q] : 0;
+        wave_lds_sync();
+        store_tile(im_tile, io.obs + e0 * O, (int64_t)nvalid * O, lane);
+        return;
+    }
+    // PTRS right-hand-side table -> LDS (after the obs tile), so the demand
+    // draw's lookups do not queue behind the step's global loads (vmcnt is in order)
+    // (fixed count of clamped loads issued first, written to LDS after the state
+    // loads are in flight)
+    // loads in the order their values are needed: period scalars, RHS table, PCG64, state
+    const int t0 = TU ? t_u : (valid ? P.cm.period[e] : 0);   // padded lanes: any in-range period
+    const int tc = t0 < P.periods ? t0 : 0;
+    const double apow0 = P.alpha_pow[tc];
+    const int64_t udem0 = P.user_D[tc];
+    double *rhs_l = reinterpret_cast<double *>(im_tile + (int64_t)EPW * O);
+    TableStage ts;
+    ts.dst = rhs_l;
+    {
+        const bool has_tab = P.pc.nk > 0;
+        const double *tsrc = has_tab ? P.rhs : P.alpha_pow;   // any valid pointer
+        const int qm = has_tab ? P.pc.nk - 1 : 0;
+#pragma unroll
+        for (int u = 0; u < TableStage::NT; u++) ts.v[u] = tsrc[min(lane + u * WAVE, qm)];
+    }
+
+    // state rows are Npad wide, so every lane loads unconditionally (straight-line
+    // loads keep the compiler's vmcnt waits exact); lanes past N take the last
+    // env's PCG64 stream (an all-zero stream would never leave the PTRS loop)
+    ImState<M1, BACKLOG> st;
+    st.g = P.cm.rng.load(valid ? e : N - 1);
+#pragma unroll
+    for (int i = 0; i < M1; i++) st.I[i] = P.I[i * S + e];
+#pragma unroll
+    for (int q = 0; q <= M1; q++) st.B[q] = BACKLOG ? P.B[q * S + e] : 0;
+    int t = t0;
+    bool fault = false;
+    if (ONE) {
+        im_launch_step<M1, BACKLOG, TU>(P, io, 0, e, e0, lane, valid, nvalid, st, t, fault, im_tile, trow, rhs_l,
+                                        &ts, &apow0, &udem0);
+    } else {
+        ts.flush(lane);
+        for (int k = 0; k < io.K; k++)
+            im_launch_step<M1, BACKLOG, false>(P, io, k, e, e0, lane, valid, nvalid, st, t, fault, im_tile, trow,
+                                               rhs_l, nullptr, nullptr, nullptr);
     }
     if (valid && leader) {
         P.cm.rng.store_state(e, st.g);
 #pragma unroll
-        for (int i = 0; i < M1; i++) P.I[i * S + e] = st.I[i];
+        for (int i = 0; i < M1; i++) st_store(P.I + i * S + e, st.I[i]);
         if (BACKLOG) {
 #pragma unroll
-            for (int q = 0; q <= M1; q++) P.B[q * S + e] = st.B[q];
+            for (int q = 0; q <= M1; q++) st_store(P.B + q * S + e, st.B[q]);
         }
         if (!TU) P.cm.period[e] = t;
         if (fault) atomicOr(P.cm.status, 1u);
     }
+    TWAIT();
+    TPROBE(5);
 }
 
 template <int M1, bool BACKLOG>
@@ -323,14 +424,21 @@ inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / b
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u,
                          const StepIO<int64_t, int64_t> &io, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
-    const size_t lds = (size_t)EPW * M1 * (p.lt_max + 1) * sizeof(int64_t);
+    const size_t lds = (size_t)EPW * M1 * (p.lt_max + 1) * sizeof(int64_t) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
-#define L_(M, B)                                                                              \
-    do {                                                                                      \
-        if (t_u >= 0)                                                                         \
-            hipLaunchKernelGGL((im_run_kernel<M, B, true>), grid, block, lds, s, p, t_u, io); \
-        else                                                                                  \
-            hipLaunchKernelGGL((im_run_kernel<M, B, false>), grid, block, lds, s, p, t_u, io);\
+#define L_(M, B)                                                                                      \
+    do {                                                                                              \
+        if (io.K == 1) {                                                                              \
+            if (t_u >= 0)                                                                             \
+                hipLaunchKernelGGL((im_run_kernel<M, B, true, true>), grid, block, lds, s, p, t_u, io);  \
+            else                                                                                      \
+                hipLaunchKernelGGL((im_run_kernel<M, B, false, true>), grid, block, lds, s, p, t_u, io); \
+        } else {                                                                                      \
+            if (t_u >= 0)                                                                             \
+                hipLaunchKernelGGL((im_run_kernel<M, B, true, false>), grid, block, lds, s, p, t_u, io); \
+            else                                                                                      \
+                hipLaunchKernelGGL((im_run_kernel<M, B, false, false>), grid, block, lds, s, p, t_u, io);\
+        }                                                                                             \
     } while (0)
     IM_DISPATCH(M1, backlog, L_)
 #undef L_
@@ -348,3 +456,9 @@ hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_
 }
 
 }  // namespace invsim
+
+#ifdef INVSIM_TIMING
+extern "C" int invsim_debug_timing(void *dst, int64_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_tbuf), (size_t)bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif

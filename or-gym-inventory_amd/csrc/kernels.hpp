@@ -14,6 +14,30 @@ namespace invsim {
 
 enum { AR_NEXT_STEP = 0, AR_SAME_STEP = 1, AR_DISABLED = 2 };
 
+// Profiling-only per-wave phase timestamps (`make timing`; never in the shipped
+// library): lane 0 of wave b writes s_memrealtime (100 MHz) for probe i to
+// g_tbuf[b][i]; probe 7 holds (XCC_ID << 32) | HW_ID.
+#ifdef INVSIM_TIMING
+constexpr int TB_WAVES = 4096, TB_PROBES = 8;
+#define TPROBE(i)                                                                              \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < TB_WAVES)                                         \
+            g_tbuf[blockIdx.x * TB_PROBES + (i)] = __builtin_amdgcn_s_memrealtime();           \
+    } while (0)
+#define TPROBE_ID()                                                                            \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < TB_WAVES)                                         \
+            g_tbuf[blockIdx.x * TB_PROBES + 7] =                                               \
+                ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |                 \
+                (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                           \
+    } while (0)
+#define TWAIT() __builtin_amdgcn_s_waitcnt(0)
+#else
+#define TPROBE(i) do {} while (0)
+#define TPROBE_ID() do {} while (0)
+#define TWAIT() do {} while (0)
+#endif
+
 struct Common {
     int64_t N;       // envs in this handle
     int64_t Npad;    // SoA row stride (elements)
@@ -106,6 +130,7 @@ __host__ __device__ inline int next_period(int t, int horizon, int autoreset, bo
 }
 
 constexpr int WAVE = 64;          // one-wave workgroups: LDS obs tile stored with 16-B coalesced rows
+constexpr int RHS_LDS_MAX = 512;  // PTRS RHS table entries per Poisson rate (staged in LDS)
 // Lanes per env.  1 = one thread per env with the sequential sampler; GRP (4) =
 // the lane-group sampler of group_rng.hpp.  tools/poisson_bench.hip measured the
 // sequential sampler (host RHS table + f32 pre-test) 1.1-1.6x faster than the
@@ -122,21 +147,73 @@ __device__ __forceinline__ int64_t env_poisson_dyn(Pcg &g, double lam) {
     return np_poisson_dyn_grp(g, lam);
 }
 
+// Workgroups are one wave, and a wave's LDS instructions execute in issue
+// order, so ordering the tile writes before other lanes' reads needs only a
+// compiler barrier.  (__syncthreads() would also drain every outstanding
+// global load/store: s_waitcnt vmcnt(0) before the s_barrier.)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Output-stream stores (obs rows, reward, flags) are non-temporal: the caller
+// reads them in a later kernel or on the host, and streaming them past L2 leaves
+// less dirty data for the end-of-kernel write-back (measured on MI355X: +7 %
+// step, +15 % rollout throughput for InvMgmt).  State stores (st_store) stay
+// cached unless INVSIM_NT_STATE (profiling experiment).
+template <typename V>
+__device__ __forceinline__ void out_store(V *p, V v) {
+    __builtin_nontemporal_store(v, p);
+}
+template <typename V>
+__device__ __forceinline__ void st_store(V *p, V v) {
+#ifdef INVSIM_NT_STATE
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // Copy `count` elements of an LDS tile to global memory, 16 B per lane.
-template <typename T>
+// MAXIT > 0: tiles of at most MAXIT * 64 16-B chunks are copied by straight-line
+// predicated code (no loop: the compiler drains every outstanding global store,
+// s_waitcnt vmcnt(0), in front of a store loop); larger tiles use the loop.
+template <int MAXIT = 0, typename T>
 __device__ __forceinline__ void store_tile(const T *__restrict__ tile, T *__restrict__ dst,
                                            int64_t count, int lane) {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const int64_t bytes = count * (int64_t)sizeof(T);
     int64_t done = 0;
     if ((((uintptr_t)dst) & 15) == 0) {
-        const int64_t n16 = bytes >> 4;
+        const int n16 = (int)(bytes >> 4);
         const v4i *s4 = reinterpret_cast<const v4i *>(tile);
         v4i *d4 = reinterpret_cast<v4i *>(dst);
-        for (int64_t i = lane; i < n16; i += WAVE) d4[i] = s4[i];
-        done = (n16 << 4) / (int64_t)sizeof(T);
+        if (MAXIT > 0 && n16 <= MAXIT * WAVE) {
+            constexpr int MI = MAXIT > 0 ? MAXIT : 1;
+            v4i r[MI];
+#pragma unroll
+            for (int u = 0; u < MI; u++) {
+                const int i = lane + u * WAVE;
+                r[u] = s4[i < n16 ? i : n16 - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < MI; u++)
+                if (lane + u * WAVE < n16) out_store(d4 + lane + u * WAVE, r[u]);
+        } else {
+            int i = lane;
+            for (; i + 7 * WAVE < n16; i += 8 * WAVE) {   // 8 LDS reads in flight, then 8 stores
+                v4i r[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) r[u] = s4[i + u * WAVE];
+#pragma unroll
+                for (int u = 0; u < 8; u++) out_store(d4 + i + u * WAVE, r[u]);
+            }
+            for (; i < n16; i += WAVE) out_store(d4 + i, s4[i]);
+        }
+        done = ((int64_t)n16 << 4) / (int64_t)sizeof(T);
+        if (done + lane < count) out_store(dst + done + lane, tile[done + lane]);   // < 16 B tail
+        return;
     }
-    for (int64_t i = done + lane; i < count; i += WAVE) dst[i] = tile[i];
+    for (int64_t i = lane; i < count; i += WAVE) out_store(dst + i, tile[i]);
 }
 
 // launchers (return hipGetLastError() of the launch)
