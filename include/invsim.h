@@ -175,6 +175,11 @@ int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, 
  * applied).  Synchronous.  clear != 0 resets it. */
 int invsim_status(invsim_handle *h, uint32_t *flags, int32_t clear);
 
+/* Which kernel a handle runs: 0 = the generic kernel of its family, 1 / 2 =
+ * NetInvMgmt specialised at compile time for the reference's default /
+ * custom supply network (chosen at create when the graph equals one of them). */
+int invsim_kernel_variant(const invsim_handle *h, int32_t *variant);
+
 /* Optional per-step demand record (info['demand'] / D): int64 [N][demand_dim],
  * written by every subsequent step/rollout(last step) when non-NULL. */
 int invsim_set_info_demand(invsim_handle *h, int64_t *demand);

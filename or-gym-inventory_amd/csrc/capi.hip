@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -27,6 +28,10 @@ struct Field {
 
 }  // namespace
 
+namespace invsim {
+int net_spec_match(const invsim_netinvmgmt_spec &h);   // netspec.hip
+}
+
 struct invsim_handle {
     int32_t family = 0;
     int32_t device = 0;
@@ -42,6 +47,7 @@ struct invsim_handle {
     NetParams net{};
     int32_t im_m1 = 0;
     bool im_backlog = false;
+    int32_t net_spec = 0;     // NET_SPEC_*: compile-time specialised kernel for this graph
     // lock-step period tracking (see kernels.hpp next_period)
     bool t_known = true;
     int32_t t_cur = 0;
@@ -531,6 +537,10 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
         p.Y = at<double>(h, o_Y);
         p.Rring = at<double>(h, o_R);
         rc = init_period(h, s->num_periods);
+        // the reference's own graphs run the compile-time specialised kernel
+        // (INVSIM_NET_GENERIC=1 forces the generic one, for cross-checks)
+        const char *gen = std::getenv("INVSIM_NET_GENERIC");
+        h->net_spec = (gen && gen[0] == '1') ? NET_SPEC_NONE : net_spec_match(*s);
     }
     return finish_create(h, out, rc);
 }
@@ -645,7 +655,7 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         }
         case INVSIM_NETINVMGMT: {
             StepIO<float, float> io{K, (const float *)actions, (float *)obs, reward, terminated, truncated, (float *)final_obs};
-            e = net_run_launch(h->net, t_u, io, s);
+            e = h->net_spec ? net_spec_launch(h->net_spec, h->net, t_u, io, s) : net_run_launch(h->net, t_u, io, s);
             break;
         }
         default: return fail(h, INVSIM_EINVAL, "bad handle family");
@@ -677,6 +687,12 @@ int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, 
         return fail(h, INVSIM_EINVAL, "rollout does not return final_obs: use NEXT_STEP or DISABLED autoreset");
     DeviceGuard g(h->device);
     return run_steps(h, K, actions, obs, reward, terminated, truncated, nullptr, (hipStream_t)stream);
+}
+
+int invsim_kernel_variant(const invsim_handle *h, int32_t *variant) {
+    if (!h || !variant) return fail(nullptr, INVSIM_EINVAL, "null argument");
+    *variant = h->family == INVSIM_NETINVMGMT ? h->net_spec : 0;
+    return INVSIM_OK;
 }
 
 int invsim_status(invsim_handle *h, uint32_t *flags, int32_t clear) {

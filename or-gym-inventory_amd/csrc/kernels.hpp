@@ -231,6 +231,10 @@ hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u,
                          const StepIO<int64_t, int64_t> &io, hipStream_t s);
 
+// Compile-time specialised NetInvMgmt kernels for the reference's own graphs
+// (netspec.hip): which built-in topology a spec equals, and its launcher.
+enum { NET_SPEC_NONE = 0, NET_SPEC_DEFAULT = 1, NET_SPEC_CUSTOM = 2 };
+hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s);
 hipError_t net_reset_launch(const NetParams &p, const uint8_t *mask, float *obs, hipStream_t s);
 hipError_t net_run_launch(const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s);
 size_t net_lds_bytes(const NetParams &p);

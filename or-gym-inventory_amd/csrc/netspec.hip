@@ -1,0 +1,426 @@
+// NetInvMgmtMasterEnv.step / reset (network_management.py:301-635) specialised
+// at compile time for the reference's own supply networks (net_topologies.hpp:
+// the default graph of network_management.py:108-139 and the custom graph of
+// network_management_custom.py:108-145).  capi.hip selects this kernel when a
+// handle's compiled tables equal one of them, else the generic table-walking
+// kernel of netinvmgmt.hip runs.  Both produce identical results.
+//
+// With the topology constexpr, every node/link loop unrolls and every per-env
+// node/link value is a register: no table reads, no LDS scratch.  The order
+// windows live in registers aligned by AGE: w[k][a-1] = R[t-a, link k] for
+// a = 1..L_k (a = L_k is this period's arrival).  A step reads the ring once
+// (all sum L entries, masked by the period like the reference's zeroed
+// history), writes one slot per link; a K-step rollout shifts the registers
+// and stores the whole ring once at the end.
+//
+// Arithmetic order is the generic kernel's (and the reference's), term by term.
+#include "../../include/invsim.h"
+#include "kernels.hpp"
+#include "net_topologies.hpp"
+
+namespace invsim {
+namespace {
+
+__device__ __forceinline__ double max0(double x) { return (x > 0) ? x : 0.0; }
+
+template <class G>
+struct NetSt {
+    Pcg g;
+    double X[G::J];
+    double U[G::RL];
+    double Y[G::E];
+    double w[G::sumL > 0 ? G::sumL : 1];   // age-aligned order windows (see above)
+};
+
+// slot of R[t - a] in link k's ring (t - a >= 0)
+template <class G>
+__device__ __forceinline__ int ring_row(int k, int t, int a) {
+    return G::ring_off[k] + (int)((uint32_t)(t - a) % (uint32_t)G::L[k]);
+}
+
+template <class G>
+__device__ __forceinline__ void spec_reset(NetSt<G> &s, float *orow) {
+#pragma unroll
+    for (int j = 0; j < G::J; j++) s.X[j] = G::I0[j];
+#pragma unroll
+    for (int r = 0; r < G::RL; r++) s.U[r] = 0.0;
+#pragma unroll
+    for (int k = 0; k < G::E; k++) s.Y[k] = 0.0;
+#pragma unroll
+    for (int q = 0; q < G::sumL; q++) s.w[q] = 0.0;
+#pragma unroll
+    for (int r = 0; r < G::RL; r++) orow[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < G::J; j++) orow[G::RL + j] = (float)G::I0[j];
+#pragma unroll
+    for (int q = 0; q < G::sumL; q++) orow[G::RL + G::J + q] = 0.f;
+}
+
+// One step (:436-635) at period t < T; obs row into orow (LDS).  Returns the
+// reward; Rn receives R[t] (the fulfilled orders) per link.
+template <class G>
+__device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst (&pc)[G::RL], const double *rhs_l,
+                                            int t, double apow, NetSt<G> &s, const float (&act)[G::E],
+                                            float *orow, double (&Rn)[G::E], int64_t (&dem)[G::RL]) {
+    // market demand draws, retail-link order (:536-541)
+    double Dd[G::RL];
+#pragma unroll
+    for (int r = 0; r < G::RL; r++) {
+        const int64_t pd = np_poisson(s.g, pc[r], rhs_l + r * RHS_LDS_MAX);
+        Dd[r] = (double)(pd > 0 ? pd : 0);
+        dem[r] = (int64_t)Dd[r];
+    }
+    double cons[G::J];
+#pragma unroll
+    for (int j = 0; j < G::J; j++) cons[j] = 0.0;
+    // 0) orders over sorted reorder links (:448-490)
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+        const double rq = rint((double)act[k]);               // round() half-to-even
+        const double request = (rq > 0) ? rq : 0.0;            // max(0, .)
+        double f;
+        if (G::sup[k] < 0) {
+            f = request;                                       // raw material: unlimited
+        } else {
+            const int sp = G::sup[k] < 0 ? 0 : G::sup[k];
+            const double oav = max0(s.X[sp] - cons[sp]);
+            double avail = oav;
+            if (G::sup_is_factory[k]) {
+                const double mpi = G::v[sp] * oav;
+                const double mp = (mpi < G::C[sp]) ? mpi : G::C[sp];   // min(C, v*avail)
+                avail = (mp < avail) ? mp : avail;
+            }
+            f = (avail < request) ? avail : request;           // min(request, avail)
+            cons[sp] += f / G::v[sp];
+        }
+        Rn[k] = f;
+    }
+    // 1) pipeline (:494-511): arrival = R[t-L] (age L), or R[t] when L == 0
+    double arrv[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+        arrv[k] = (G::L[k] == 0) ? Rn[k] : s.w[G::ring_off[k] + (G::L[k] > 0 ? G::L[k] : 1) - 1];
+        s.Y[k] = s.Y[k] - arrv[k] + Rn[k];
+    }
+    // arrivals in predecessor adjacency order (:516-523); X[t+1] (:528)
+#pragma unroll
+    for (int j = 0; j < G::J; j++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = G::pred_ptr[j]; q < G::pred_ptr[j + 1]; q++) acc += arrv[G::pred_idx[q]];
+        s.X[j] = (s.X[j] + acc) - cons[j];
+    }
+    // 2&3) market fulfilment in retail-link edge order (:536-566)
+    double Sr[G::RL];
+#pragma unroll
+    for (int r = 0; r < G::RL; r++) {
+        const double fill = Dd[r] + s.U[r];
+        const int node = G::rl_node[r];
+        const double inv = max0(s.X[node]);
+        const double sale = (inv < fill) ? inv : fill;          // min(fill, inv)
+        s.X[node] -= sale;
+        Sr[r] = sale;
+        s.U[r] = P.backlog ? fill - sale : 0.0;
+    }
+    // 5) profit per main node (:578-613), Python sum() order = adjacency order
+    double total = 0.0;
+#pragma unroll
+    for (int j = 0; j < G::J; j++) {
+        double SR = 0.0, sold = 0.0;
+#pragma unroll
+        for (int q = G::succ_ptr[j]; q < G::succ_ptr[j + 1]; q++) {
+            const int idx = G::succ_idx[q];
+            const bool re = G::succ_kind[q] == 0;
+            const double sv = re ? Rn[idx < G::E ? idx : 0] : Sr[idx < G::RL ? idx : 0];
+            SR += (re ? G::lp[idx < G::E ? idx : 0] : G::rl_p[idx < G::RL ? idx : 0]) * sv;
+            sold += sv;
+        }
+        double PC = 0.0, HCp = 0.0;
+#pragma unroll
+        for (int q = G::pred_ptr[j]; q < G::pred_ptr[j + 1]; q++) PC += G::lp[G::pred_idx[q]] * Rn[G::pred_idx[q]];
+        const double HC_on = G::h[j] * max0(s.X[j]);
+#pragma unroll
+        for (int q = G::pred_ptr[j]; q < G::pred_ptr[j + 1]; q++) HCp += G::lg[G::pred_idx[q]] * max0(s.Y[G::pred_idx[q]]);
+        const double HC = HC_on + HCp;
+        double OC = 0.0;
+        if (G::is_factory[j]) OC = (G::v[j] > 0) ? G::o[j] * (sold / G::v[j]) : 0.0;
+        double UP = 0.0;
+        if (G::is_retail[j]) {
+#pragma unroll
+            for (int q = G::succ_ptr[j]; q < G::succ_ptr[j + 1]; q++)
+                if (G::succ_kind[q] == 1) UP += G::rl_b[G::succ_idx[q] < G::RL ? G::succ_idx[q] : 0] *
+                                                s.U[G::succ_idx[q] < G::RL ? G::succ_idx[q] : 0];
+        }
+        total += SR - PC - OC - HC - UP;
+    }
+    // obs (:334-413): U[t+1], X[t+1], then per link with L > 0 the fulfilled
+    // orders R[t+1-L .. t] oldest first (ages L-1 .. 1, then R[t])
+#pragma unroll
+    for (int r = 0; r < G::RL; r++) orow[r] = (float)s.U[r];
+#pragma unroll
+    for (int j = 0; j < G::J; j++) orow[G::RL + j] = (float)s.X[j];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+        if (G::L[k] == 0) continue;
+#pragma unroll
+        for (int p = 0; p + 1 < G::L[k]; p++)
+            orow[G::win_off[k] + p] = (float)s.w[G::ring_off[k] + (G::L[k] - 1 - p) - 1];
+        orow[G::win_off[k] + G::L[k] - 1] = (float)Rn[k];
+    }
+    (void)t;
+    return apow * total;                                       // :619
+}
+
+// shift the age-aligned windows by one period: age a+1 <- age a, age 1 <- R[t]
+template <class G>
+__device__ __forceinline__ void spec_shift(NetSt<G> &s, const double (&Rn)[G::E]) {
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+        if (G::L[k] == 0) continue;
+#pragma unroll
+        for (int a = G::L[k]; a >= 2; a--) s.w[G::ring_off[k] + a - 1] = s.w[G::ring_off[k] + a - 2];
+        s.w[G::ring_off[k]] = Rn[k];
+    }
+}
+
+template <class G, bool TU, bool ONE>
+__global__ void __launch_bounds__(WAVE)
+net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io) {
+    extern __shared__ __attribute__((aligned(16))) float ns_lds[];
+    constexpr int O = G::O;
+    constexpr int TILE_IT = (EPW * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
+    const int lane = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * EPW;
+    const int64_t e = e0 + lane;
+    const int64_t N = P.cm.N;
+    const bool valid = e < N;
+    const int nvalid = (int)((N - e0) < EPW ? (N - e0) : EPW);
+    const int64_t S = P.cm.Npad;
+    const int64_t el = valid ? e : N - 1;      // lanes past N mirror env N-1 (loads only)
+    float *tile = ns_lds;
+    float *trow = tile + lane * O;
+    double *rhs_l = reinterpret_cast<double *>(ns_lds + ((EPW * O + 3) / 4) * 4);
+
+    int t = TU ? t_u : P.cm.period[el];
+    NetSt<G> st;
+    if (ONE && TU && t >= P.T) {
+        // lock-step NEXT_STEP autoreset of the whole batch (the host refuses a
+        // DISABLED overrun when lock-step; SAME_STEP resets in the done step)
+        spec_reset<G>(st, trow);
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < G::J; j++) P.X[j * S + e] = G::I0[j];
+#pragma unroll
+            for (int r = 0; r < G::RL; r++) P.U[r * S + e] = 0.0;
+#pragma unroll
+            for (int k = 0; k < G::E; k++) P.Y[k * S + e] = 0.0;
+            out_store(io.rew + e, 0.0);
+            out_store(io.term + e, (uint8_t)0);
+            out_store(io.trunc + e, (uint8_t)0);
+        }
+        wave_lds_sync();
+        store_tile<TILE_IT>(tile, io.obs + e0 * O, (int64_t)nvalid * O, lane);
+        return;
+    }
+    // every load up front, in the order the values are needed
+    const int tc = (t < P.T) ? t : 0;
+    double apow = P.alpha_pow[tc];
+    PtrsConst pc[G::RL];
+#pragma unroll
+    for (int r = 0; r < G::RL; r++) pc[r] = P.rl_pc[r];
+    constexpr int NT = RHS_LDS_MAX / WAVE;
+    double tv[G::RL][NT];
+#pragma unroll
+    for (int r = 0; r < G::RL; r++) {
+        const int qm = pc[r].nk > 0 ? pc[r].nk - 1 : 0;
+        const double *src = pc[r].nk > 0 ? P.rhs + pc[r].toff : P.alpha_pow;   // any valid pointer
+#pragma unroll
+        for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
+    }
+    st.g = P.cm.rng.load(el);
+#pragma unroll
+    for (int j = 0; j < G::J; j++) st.X[j] = P.X[j * S + el];
+#pragma unroll
+    for (int r = 0; r < G::RL; r++) st.U[r] = P.U[r * S + el];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) st.Y[k] = P.Y[k * S + el];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+        if (G::L[k] == 0) continue;
+#pragma unroll
+        for (int a = 1; a <= G::L[k]; a++) {
+            const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+            const double v = P.Rring[(int64_t)row * S + el];
+            st.w[G::ring_off[k] + a - 1] = (t - a >= 0) ? v : 0.0;   // zeroed history (:315-321)
+        }
+    }
+    float act[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) act[k] = io.act[el * G::E + k];
+#pragma unroll
+    for (int r = 0; r < G::RL; r++)
+#pragma unroll
+        for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
+    wave_lds_sync();
+
+    bool fault = false;
+    bool dirty_all = false;                    // rollout: whole ring rewritten at the end
+    const int t_start = t;
+    double Rn[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) Rn[k] = 0.0;
+    const int K = ONE ? 1 : io.K;
+    for (int kk = 0; kk < K; kk++) {
+        const int64_t oi = (int64_t)kk * N + e;
+        if (kk > 0) {
+            const int64_t ea = (int64_t)kk * N + el;
+#pragma unroll
+            for (int k = 0; k < G::E; k++) act[k] = io.act[ea * G::E + k];
+            apow = P.alpha_pow[(t < P.T) ? t : 0];
+        }
+        bool tr = false;
+        if (!(ONE && TU) && t >= P.T) {
+            if (P.cm.autoreset == AR_NEXT_STEP) {
+                spec_reset<G>(st, trow);
+                dirty_all = true;
+                if (valid) {
+                    out_store(io.rew + oi, 0.0);
+                    out_store(io.term + oi, (uint8_t)0);
+                    out_store(io.trunc + oi, (uint8_t)0);
+                }
+                t = 0;
+            } else {
+                fault = true;   // stepping past the horizon (DISABLED)
+            }
+        } else {
+            int64_t dem[G::RL];
+            const double r = spec_step<G>(P, pc, rhs_l, t, apow, st, act, trow, Rn, dem);
+            tr = t + 1 >= P.T;
+            if (valid) {
+                out_store(io.rew + oi, r);
+                out_store(io.term + oi, (uint8_t)0);
+                out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
+                if (kk == K - 1 && P.cm.info_demand) {
+#pragma unroll
+                    for (int q = 0; q < G::RL; q++) P.cm.info_demand[e * G::RL + q] = dem[q];
+                }
+            }
+            if (ONE) {
+                // single step: the ring changes in one slot per link, R[t]
+                if (valid) {
+#pragma unroll
+                    for (int k = 0; k < G::E; k++)
+                        if (G::L[k] > 0)
+                            st_store(P.Rring + (int64_t)(G::ring_off[k] + (int)((uint32_t)t % (uint32_t)G::L[k])) * S + e,
+                                     Rn[k]);
+                }
+            } else {
+                spec_shift<G>(st, Rn);
+                dirty_all = true;
+            }
+            t += 1;
+        }
+        if (P.cm.autoreset == AR_SAME_STEP && tr) {          // final obs out, then the reset obs in
+            wave_lds_sync();
+            if (valid && io.fobs)
+                for (int q = 0; q < O; q++) io.fobs[e * O + q] = trow[q];
+            wave_lds_sync();
+            spec_reset<G>(st, trow);
+            dirty_all = true;
+            t = 0;
+        }
+        wave_lds_sync();
+        store_tile<TILE_IT>(tile, io.obs + ((int64_t)kk * N + e0) * O, (int64_t)nvalid * O, lane);
+        wave_lds_sync();
+    }
+    if (valid) {
+        P.cm.rng.store_state(e, st.g);
+#pragma unroll
+        for (int j = 0; j < G::J; j++) st_store(P.X + j * S + e, st.X[j]);
+#pragma unroll
+        for (int r = 0; r < G::RL; r++) st_store(P.U + r * S + e, st.U[r]);
+#pragma unroll
+        for (int k = 0; k < G::E; k++) st_store(P.Y + k * S + e, st.Y[k]);
+        if (!ONE && dirty_all) {
+            // ring slot of R[t - a] = age-a window register (zeros before the episode)
+#pragma unroll
+            for (int k = 0; k < G::E; k++) {
+                if (G::L[k] == 0) continue;
+#pragma unroll
+                for (int a = 1; a <= G::L[k]; a++)
+                    st_store(P.Rring + (int64_t)(G::ring_off[k] +
+                                                 (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k])) * S + e,
+                             st.w[G::ring_off[k] + a - 1]);
+            }
+        }
+        if (!TU) P.cm.period[e] = t;
+        if (fault) atomicOr(P.cm.status, 1u);
+    }
+    (void)t_start;
+}
+
+}  // namespace
+
+template <class G>
+static bool topo_eq(const invsim_netinvmgmt_spec &h) {
+    if (h.n_main != G::J || h.n_reorder != G::E || h.n_retail != G::RL) return false;
+    for (int j = 0; j < G::J; j++)
+        if (h.I0[j] != G::I0[j] || h.h[j] != G::h[j] || h.C[j] != G::C[j] || h.o[j] != G::o[j] ||
+            h.v[j] != G::v[j] || h.is_factory[j] != G::is_factory[j] || h.is_retail[j] != G::is_retail[j])
+            return false;
+    for (int k = 0; k < G::E; k++)
+        if (h.sup[k] != G::sup[k] || h.pur[k] != G::pur[k] || h.sup_is_factory[k] != G::sup_is_factory[k] ||
+            h.L[k] != G::L[k] || h.lp[k] != G::lp[k] || h.lg[k] != G::lg[k])
+            return false;
+    for (int r = 0; r < G::RL; r++)
+        if (h.rl_node[r] != G::rl_node[r] || h.rl_p[r] != G::rl_p[r] || h.rl_b[r] != G::rl_b[r] ||
+            h.rl_user[r] != 0)
+            return false;
+    for (int j = 0; j <= G::J; j++)
+        if (h.succ_ptr[j] != G::succ_ptr[j] || h.pred_ptr[j] != G::pred_ptr[j]) return false;
+    for (int q = 0; q < G::NSUCC; q++)
+        if (h.succ_kind[q] != G::succ_kind[q] || h.succ_idx[q] != G::succ_idx[q]) return false;
+    for (int q = 0; q < G::NPRED; q++)
+        if (h.pred_idx[q] != G::pred_idx[q]) return false;
+    return true;
+}
+
+int net_spec_match(const invsim_netinvmgmt_spec &h) {
+    if (topo_eq<NetTopoDefault>(h)) return NET_SPEC_DEFAULT;
+    if (topo_eq<NetTopoCustom>(h)) return NET_SPEC_CUSTOM;
+    return NET_SPEC_NONE;
+}
+
+template <class G>
+static size_t spec_lds_bytes() {
+    return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float) + (size_t)G::RL * RHS_LDS_MAX * sizeof(double);
+}
+
+template <class G>
+static hipError_t spec_launch(const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s) {
+    const size_t lds = spec_lds_bytes<G>();
+    const dim3 grid((unsigned)((p.cm.N + EPW - 1) / EPW)), block(WAVE);
+    if (io.K == 1) {
+        if (t_u >= 0)
+            hipLaunchKernelGGL((net_spec_kernel<G, true, true>), grid, block, lds, s, p, t_u, io);
+        else
+            hipLaunchKernelGGL((net_spec_kernel<G, false, true>), grid, block, lds, s, p, t_u, io);
+    } else {
+        if (t_u >= 0)
+            hipLaunchKernelGGL((net_spec_kernel<G, true, false>), grid, block, lds, s, p, t_u, io);
+        else
+            hipLaunchKernelGGL((net_spec_kernel<G, false, false>), grid, block, lds, s, p, t_u, io);
+    }
+    return hipGetLastError();
+}
+
+hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s) {
+    if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
+    switch (which) {
+        case NET_SPEC_DEFAULT: return spec_launch<NetTopoDefault>(p, t_u, io, s);
+        case NET_SPEC_CUSTOM: return spec_launch<NetTopoCustom>(p, t_u, io, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace invsim

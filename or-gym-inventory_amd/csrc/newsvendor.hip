@@ -1,5 +1,5 @@
 // NewsvendorEnv.step / reset (newsvendor.py:100-204) as HIP kernels for
-// gfx950: one wave = 16 envs x 4 lanes (group_rng.hpp), K steps per launch.
+// gfx950: one wave of 64 envs (one per lane) per workgroup, K steps per launch.
 //
 // Per-env HBM state (SoA rows of Npad): params price,cost,h,k,mu (f64: they
 // are Python floats in the reference), the order pipeline as a ring of L f32
@@ -87,7 +87,7 @@ __device__ __forceinline__ void nv_reset_regs(const NvParams &P, int64_t e, NvSt
 
 // One newsvendor.py:125-204 step at step count sc.  Returns truncated.
 template <int LT>
-__device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, int sc, NvState<LT> &s,
+__device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool valid, int sc, NvState<LT> &s,
                                              float action, float *orow, double &reward, int64_t *dem) {
     const int64_t S = P.cm.Npad;
     const int L = (LT >= 0) ? LT : P.L;
@@ -123,7 +123,7 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, int s
         for (int p = 0; p + 1 < L; p++) orow[5 + p] = pos(p + 1);
         if (L > 0) orow[5 + L - 1] = qf;
     }
-    if (L > 0 && orow) P.pipe[(int64_t)base * S + e] = qf;                 // leader: replaces the arrived slot
+    if (L > 0 && valid) P.pipe[(int64_t)base * S + e] = qf;                // replaces the arrived slot
     if (LT > 0) {
 #pragma unroll
         for (int p = 0; p + 1 < (LT > 0 ? LT : 1); p++) s.pv[p] = s.pv[p + 1];
@@ -134,7 +134,7 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, int s
     return sc + 1 >= P.step_limit;                                          // :190
 }
 
-template <int LT, bool TU>
+template <int LT, bool TU, bool ONE>
 __global__ void __launch_bounds__(WAVE)
 nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
     extern __shared__ __attribute__((aligned(16))) float nv_tile[];
@@ -147,59 +147,79 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
     const int nvalid = (int)((N - e0) < EPW ? (N - e0) : EPW);
     const int O = P.L + 5;
     const int64_t S = P.cm.Npad;
-    float *trow = leader ? nv_tile + (int64_t)(lane / LPE) * O : nullptr;  // leader writes obs/state
+    float *trow = nv_tile + (int64_t)(lane / LPE) * O;
+    // obs tile of at most 64 x (16 + 5) f32 in the compile-time lead-time variants
+    constexpr int TILE_IT = (EPW * 21 * 4 + 16 * WAVE - 1) / (16 * WAVE);
+    // lanes past N mirror env N-1 (loads only; they store nothing): straight-line
+    // loads keep the compiler's waits exact, and a real PCG64 stream / rate keeps
+    // the Poisson loop finite
+    const int64_t el = valid ? e : N - 1;
 
     NvState<LT> st;
-    int sc = t_u;
-    if (valid) {
-        st.g = P.cm.rng.load(e);
-#pragma unroll
-        for (int j = 0; j < 5; j++) st.par[j] = P.par[j * S + e];
-        if (!TU) sc = P.cm.period[e];
-        if (LT > 0) {
-            const int base = (int)((uint32_t)(sc + 1) % (uint32_t)(LT > 0 ? LT : 1));
-#pragma unroll
-            for (int p = 0; p < (LT > 0 ? LT : 1); p++) {
-                int sl = base + p;
-                sl = sl >= LT ? sl - LT : sl;
-                st.pv[p] = (p >= LT - sc) ? P.pipe[(int64_t)sl * S + e] : 0.f;
-            }
-        }
-    }
-    for (int k = 0; k < io.K; k++) {
-        const int64_t oi = (int64_t)k * N + e;
+    st.g = P.cm.rng.load(el);
+    int sc = TU ? t_u : P.cm.period[el];
+    if (ONE && TU && sc >= P.step_limit) {
+        // lock-step NEXT_STEP autoreset of the whole batch (DISABLED overruns are
+        // refused by the host when lock-step; SAME_STEP resets in the done step)
+        nv_reset_regs<LT>(P, e, st, trow, valid);
         if (valid) {
-            if (P.cm.autoreset == AR_NEXT_STEP && sc >= P.step_limit) {
-                nv_reset_regs<LT>(P, e, st, trow, leader);
-                if (leader) {
-                    io.rew[oi] = 0.0;
-                    io.term[oi] = 0;
-                    io.trunc[oi] = 0;
-                }
+            out_store(io.rew + e, 0.0);
+            out_store(io.term + e, (uint8_t)0);
+            out_store(io.trunc + e, (uint8_t)0);
+            P.cm.rng.store_state(e, st.g);
+        }
+        wave_lds_sync();
+        store_tile<TILE_IT>(nv_tile, io.obs + e0 * O, (int64_t)nvalid * O, lane);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 5; j++) st.par[j] = P.par[j * S + el];
+    if (LT > 0) {
+        const int base = (int)((uint32_t)(sc + 1) % (uint32_t)(LT > 0 ? LT : 1));
+#pragma unroll
+        for (int p = 0; p < (LT > 0 ? LT : 1); p++) {
+            int sl = base + p;
+            sl = sl >= LT ? sl - LT : sl;
+            st.pv[p] = P.pipe[(int64_t)sl * S + el];
+            if (!(p >= LT - sc)) st.pv[p] = 0.f;
+        }
+    }
+    const int K = ONE ? 1 : io.K;
+    for (int k = 0; k < K; k++) {
+        const int64_t oi = (int64_t)k * N + e;
+        const float act = io.act[(int64_t)k * N + el];
+        if (!(ONE && TU) && P.cm.autoreset == AR_NEXT_STEP && sc >= P.step_limit) {
+            nv_reset_regs<LT>(P, e, st, trow, valid);
+            if (valid) {
+                out_store(io.rew + oi, 0.0);
+                out_store(io.term + oi, (uint8_t)0);
+                out_store(io.trunc + oi, (uint8_t)0);
+            }
+            sc = 0;
+        } else {
+            double r;
+            const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, r,
+                                             (valid && k == K - 1) ? P.cm.info_demand : nullptr);
+            if (valid) {
+                out_store(io.rew + oi, r);
+                out_store(io.term + oi, (uint8_t)0);
+                out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
+            }
+            sc += 1;
+            if (tr && P.cm.autoreset == AR_SAME_STEP) {
+                wave_lds_sync();
+                if (io.fobs && valid)
+                    for (int j = 0; j < O; j++) io.fobs[e * O + j] = trow[j];
+                wave_lds_sync();
+                nv_reset_regs<LT>(P, e, st, trow, valid);
                 sc = 0;
-            } else {
-                double r;
-                const bool tr = nv_step_regs<LT>(P, e, sc, st, io.act[oi], trow, r,
-                                                 (leader && k == io.K - 1) ? P.cm.info_demand : nullptr);
-                if (leader) {
-                    io.rew[oi] = r;
-                    io.term[oi] = 0;
-                    io.trunc[oi] = tr ? 1 : 0;
-                }
-                sc += 1;
-                if (tr && P.cm.autoreset == AR_SAME_STEP) {
-                    if (io.fobs && leader)
-                        for (int j = 0; j < O; j++) io.fobs[e * O + j] = trow[j];
-                    nv_reset_regs<LT>(P, e, st, trow, leader);
-                    sc = 0;
-                }
             }
         }
-        __syncthreads();
-        store_tile(nv_tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
-        __syncthreads();
+        wave_lds_sync();
+        store_tile<TILE_IT>(nv_tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+        wave_lds_sync();
     }
-    if (valid && leader) {
+    if (valid) {
         P.cm.rng.store_state(e, st.g);
         if (!TU) P.cm.period[e] = sc;
     }
@@ -225,12 +245,19 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const StepIO<float, float> 
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = (size_t)EPW * (p.L + 5) * sizeof(float);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
-#define L_(X)                                                                                 \
-    do {                                                                                      \
-        if (t_u >= 0)                                                                         \
-            hipLaunchKernelGGL((nv_run_kernel<X, true>), grid, block, lds, s, p, t_u, io);    \
-        else                                                                                  \
-            hipLaunchKernelGGL((nv_run_kernel<X, false>), grid, block, lds, s, p, t_u, io);   \
+#define L_(X)                                                                                       \
+    do {                                                                                            \
+        if (io.K == 1) {                                                                            \
+            if (t_u >= 0)                                                                           \
+                hipLaunchKernelGGL((nv_run_kernel<X, true, true>), grid, block, lds, s, p, t_u, io);  \
+            else                                                                                    \
+                hipLaunchKernelGGL((nv_run_kernel<X, false, true>), grid, block, lds, s, p, t_u, io); \
+        } else {                                                                                    \
+            if (t_u >= 0)                                                                           \
+                hipLaunchKernelGGL((nv_run_kernel<X, true, false>), grid, block, lds, s, p, t_u, io); \
+            else                                                                                    \
+                hipLaunchKernelGGL((nv_run_kernel<X, false, false>), grid, block, lds, s, p, t_u, io);\
+        }                                                                                           \
     } while (0)
     switch (p.L) {
         case 0: L_(0); break;

@@ -22,7 +22,8 @@ EXPORTS = (
     "invsim_abi_version", "invsim_last_error", "invsim_create_newsvendor",
     "invsim_create_invmgmt", "invsim_create_netinvmgmt", "invsim_destroy", "invsim_dims",
     "invsim_set_autoreset", "invsim_seed_range", "invsim_seed_words", "invsim_reset",
-    "invsim_step", "invsim_rollout", "invsim_status", "invsim_set_info_demand", "invsim_state_bytes",
+    "invsim_step", "invsim_rollout", "invsim_status", "invsim_kernel_variant", "invsim_set_info_demand",
+    "invsim_state_bytes",
     "invsim_state_field", "invsim_get_state", "invsim_set_state",
 )
 
@@ -78,6 +79,7 @@ def _declare(lib):
         "invsim_step": ([H, P, P, P, P, P, P, P], C.c_int),
         "invsim_rollout": ([H, I32, P, P, P, P, P, P], C.c_int),
         "invsim_status": ([H, P, I32], C.c_int),
+        "invsim_kernel_variant": ([H, P], C.c_int),
         "invsim_set_info_demand": ([H, P], C.c_int),
         "invsim_state_bytes": ([H, P], C.c_int),
         "invsim_state_field": ([H, I32, P, P, P, P, P], C.c_int),

@@ -228,6 +228,14 @@ class InvSimVectorEnv:
         _capi.check(self._lib.invsim_status(self._h, _capi.C.byref(f), int(clear)), self._h, "status")
         return f.value
 
+    @property
+    def kernel_variant(self):
+        """0 = generic kernel; 1 / 2 = NetInvMgmt kernel specialised for the
+        reference's default / custom supply network."""
+        v = _capi.C.c_int32()
+        _capi.check(self._lib.invsim_kernel_variant(self._h, _capi.C.byref(v)), self._h, "kernel_variant")
+        return v.value
+
     # -- state -----------------------------------------------------------------
     def state_bytes(self):
         b = _capi.C.c_int64()
