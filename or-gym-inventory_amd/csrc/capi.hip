@@ -246,10 +246,17 @@ int invsim_create_newsvendor(const invsim_newsvendor_spec *spec, int64_t n, int3
     common_fields(h, lay, o_rng, o_per, o_st);
     int64_t o_par = lay.add("params", 8, 5, h->Npad);
     int64_t o_pipe = lay.add("pipeline", 4, std::max(L, 1), h->Npad);
+    // loggam(k + 1) for the per-env PTRS right-hand side (numpy's formula, host libm)
+    Blob tb;
+    std::vector<double> lg(RHS_LDS_MAX);
+    for (int k = 0; k < RHS_LDS_MAX; k++) lg[k] = np_loggam((double)(k + 1));
+    const int64_t t_lg = tb.put(lg.data(), lg.size());
     int rc = alloc_arena(h, lay);
+    if (rc == INVSIM_OK) rc = upload_tables(h, tb.b);
     if (rc == INVSIM_OK) {
         bind_common(h, o_rng, o_per, o_st, ar);
         NvParams &p = h->nv;
+        p.lgtab = tab<double>(h, t_lg);
         p.cm = h->cm;
         p.L = L;
         p.step_limit = spec->step_limit;

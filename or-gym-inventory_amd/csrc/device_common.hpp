@@ -214,6 +214,43 @@ __device__ __forceinline__ int64_t np_poisson(Pcg &g, const PtrsConst &c, const 
     return np_poisson_mult(g, c.enlam);
 }
 
+// numpy random_poisson_ptrs for a per-env lam with a (lam-independent) table of
+// loggam(k + 1), k < lgn, computed on the host with numpy's own formula
+__device__ inline int64_t np_poisson_ptrs_lg(Pcg &g, const PtrsConst &c, const double *lgtab, int lgn) {
+    for (;;) {
+        double U = g.next_double() - 0.5;
+        double V = g.next_double();
+        double us = 0.5 - fabs(U);
+        int64_t k = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+        if ((us >= 0.07) && (V <= c.vr)) return k;
+        if ((k < 0) || ((us < 0.013) && (V > us))) continue;
+        const double r = (k < lgn) ? (-c.lam + (double)k * c.loglam) - lgtab[k < lgn ? k : 0]
+                                   : -c.lam + (double)k * c.loglam - np_loggam((double)(k + 1));
+        if (ptrs_log_accept(c, V, us, r)) return k;
+    }
+}
+
+// numpy random_poisson for a per-env lam: only the branch's constants are computed
+__device__ inline int64_t np_poisson_dyn(Pcg &g, double lam, const double *lgtab, int lgn) {
+    if (lam >= 10) {
+        PtrsConst c;
+        c.lam = lam;
+        c.slam = sqrt(lam);
+        c.loglam = log(lam);
+        c.b = 0.931 + 2.53 * c.slam;
+        c.a = -0.059 + 0.02483 * c.b;
+        c.invalpha = 1.1239 + 1.1328 / (c.b - 3.4);
+        c.vr = 0.9277 - 3.6224 / (c.b - 2);
+        c.log_invalpha = log(c.invalpha);
+        c.a2 = 2 * c.a;
+        c.k0 = 0;
+        c.nk = 0;
+        return np_poisson_ptrs_lg(g, c, lgtab, lgn);
+    }
+    if (lam == 0) return 0;
+    return np_poisson_mult(g, exp(-lam));
+}
+
 // numpy random_poisson for a per-env lam: only the branch's constants are computed
 __device__ inline int64_t np_poisson_dyn(Pcg &g, double lam) {
     if (lam >= 10) {

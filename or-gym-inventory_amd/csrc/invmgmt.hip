@@ -49,20 +49,6 @@ __device__ __forceinline__ int64_t min_via_f64(int64_t a, int64_t sup) {
     return (int64_t)((x <= y) ? x : y);
 }
 
-// PTRS RHS table values loaded by each lane, written to the LDS table once the
-// step's global loads are all in flight (a wait for these loads would
-// otherwise hold back every load issued after it)
-struct TableStage {
-    static constexpr int NT = RHS_LDS_MAX / WAVE;
-    double *dst;
-    double v[NT];
-    __device__ __forceinline__ void flush(int lane) {
-#pragma unroll
-        for (int u = 0; u < NT; u++) dst[lane + u * WAVE] = v[u];
-        __builtin_amdgcn_wave_barrier();
-    }
-};
-
 template <int M1, bool BACKLOG>
 struct ImState {
     Pcg g;
@@ -240,6 +226,10 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
     const int O = M1 * (P.lt_max + 1);
     const int64_t oi = (int64_t)k * N + e;
     bool tr = false;
+    if (!STEP_ONLY && ts) {   // all lanes write the table before the divergent branch
+        ts->flush(lane);
+        ts = nullptr;
+    }
     if (!STEP_ONLY && t >= P.periods) {
         if (P.cm.autoreset == AR_NEXT_STEP) {
             im_reset_regs<M1, BACKLOG>(P, st, trow, j);

@@ -56,6 +56,7 @@ struct NvParams {
     double max_inventory, max_order;
     double p_max, h_max, k_max, mu_max;
     double *par;         // [5][Npad]  price, cost, h, k, mu  (Python floats)
+    const double *lgtab; // [RHS_LDS_MAX] loggam(k + 1), host (numpy's formula)
     float *pipe;         // [L][Npad]  order ring, slot = step index mod L
 };
 
@@ -146,14 +147,39 @@ __device__ __forceinline__ int64_t env_poisson_dyn(Pcg &g, double lam) {
     if (LPE == 1) return np_poisson_dyn(g, lam);
     return np_poisson_dyn_grp(g, lam);
 }
+__device__ __forceinline__ int64_t env_poisson_dyn(Pcg &g, double lam, const double *lgtab, int lgn) {
+    return np_poisson_dyn(g, lam, lgtab, lgn);
+}
 
 // Workgroups are one wave, and a wave's LDS instructions execute in issue
 // order, so ordering the tile writes before other lanes' reads needs only a
 // compiler barrier.  (__syncthreads() would also drain every outstanding
 // global load/store: s_waitcnt vmcnt(0) before the s_barrier.)
 __device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// A RHS_LDS_MAX-entry read-only table (PTRS right-hand sides / loggam) copied to
+// LDS: each lane loads its NT entries early, and the LDS write happens once the
+// step's other global loads are in flight (a wait for these loads would
+// otherwise hold back every load issued after them: vmcnt is in order).
+struct TableStage {
+    static constexpr int NT = RHS_LDS_MAX / WAVE;
+    double *dst;
+    double v[NT];
+    __device__ __forceinline__ void load(const double *src, int n, int lane) {
+        const int qm = n > 0 ? n - 1 : 0;
+#pragma unroll
+        for (int u = 0; u < NT; u++) v[u] = src[min(lane + u * WAVE, qm)];
+    }
+    __device__ __forceinline__ void flush(int lane) {
+#pragma unroll
+        for (int u = 0; u < NT; u++) dst[lane + u * WAVE] = v[u];
+        __builtin_amdgcn_wave_barrier();
+    }
+};
 
 // Output-stream stores (obs rows, reward, flags) are non-temporal: the caller
 // reads them in a later kernel or on the host, and streaming them past L2 leaves

@@ -16,6 +16,10 @@
 namespace invsim {
 namespace {
 
+#ifdef INVSIM_TIMING
+__device__ uint64_t g_tbuf[TB_WAVES * TB_PROBES];
+#endif
+
 enum { K_PY = 0, K_F32 = 1, K_F64 = 2 };
 struct Tv {
     double v;
@@ -88,7 +92,8 @@ __device__ __forceinline__ void nv_reset_regs(const NvParams &P, int64_t e, NvSt
 // One newsvendor.py:125-204 step at step count sc.  Returns truncated.
 template <int LT>
 __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool valid, int sc, NvState<LT> &s,
-                                             float action, float *orow, double &reward, int64_t *dem) {
+                                             float action, float *orow, const double *lg_l, TableStage *ts,
+                                             double &reward, int64_t *dem) {
     const int64_t S = P.cm.Npad;
     const int L = (LT >= 0) ? LT : P.L;
     const int base = (L > 0) ? (int)((uint32_t)(sc + 1) % (uint32_t)L) : 0;  // slot of position 0
@@ -98,7 +103,10 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
         sl = sl >= L ? sl - L : sl;
         return (p >= L - sc) ? P.pipe[(int64_t)sl * S + e] : 0.f;
     };
-    const int64_t d = env_poisson_dyn(s.g, s.par[4]);                      // :146
+    if (ts) ts->flush((int)threadIdx.x);
+    TPROBE(1);
+    const int64_t d = env_poisson_dyn(s.g, s.par[4], lg_l, RHS_LDS_MAX);  // :146
+    TPROBE(2);
     const Tv ZERO = tv(0.0, K_PY);
     const Tv oq = tv(np_clip((double)action, 0.0, P.max_order), K_F64);    // :131-132
     const float S5 = np_sum<float>(L, pos);                                 // :135
@@ -131,6 +139,7 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
     }
     reward = r.v;
     if (dem) dem[e] = d;
+    TPROBE(3);
     return sc + 1 >= P.step_limit;                                          // :190
 }
 
@@ -148,6 +157,8 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
     const int O = P.L + 5;
     const int64_t S = P.cm.Npad;
     float *trow = nv_tile + (int64_t)(lane / LPE) * O;
+    TPROBE(0);
+    TPROBE_ID();
     // obs tile of at most 64 x (16 + 5) f32 in the compile-time lead-time variants
     constexpr int TILE_IT = (EPW * 21 * 4 + 16 * WAVE - 1) / (16 * WAVE);
     // lanes past N mirror env N-1 (loads only; they store nothing): straight-line
@@ -172,6 +183,10 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
         store_tile<TILE_IT>(nv_tile, io.obs + e0 * O, (int64_t)nvalid * O, lane);
         return;
     }
+    // loggam(k + 1) table -> LDS after the tile (written once the step's loads are in flight)
+    TableStage ts;
+    ts.dst = reinterpret_cast<double *>(nv_tile + ((EPW * O + 3) / 4) * 4);
+    ts.load(P.lgtab, RHS_LDS_MAX, lane);
 #pragma unroll
     for (int j = 0; j < 5; j++) st.par[j] = P.par[j * S + el];
     if (LT > 0) {
@@ -185,6 +200,9 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
         }
     }
     const int K = ONE ? 1 : io.K;
+    // all lanes write the table: before any divergent step/reset branch (with a
+    // lock-step single step there is none, and the write waits inside the step)
+    if (!(ONE && TU)) ts.flush(lane);
     for (int k = 0; k < K; k++) {
         const int64_t oi = (int64_t)k * N + e;
         const float act = io.act[(int64_t)k * N + el];
@@ -198,7 +216,7 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
             sc = 0;
         } else {
             double r;
-            const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, r,
+            const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, ts.dst, (ONE && TU) ? &ts : nullptr, r,
                                              (valid && k == K - 1) ? P.cm.info_demand : nullptr);
             if (valid) {
                 out_store(io.rew + oi, r);
@@ -217,12 +235,15 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
         }
         wave_lds_sync();
         store_tile<TILE_IT>(nv_tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+        TPROBE(4);
         wave_lds_sync();
     }
     if (valid) {
         P.cm.rng.store_state(e, st.g);
         if (!TU) P.cm.period[e] = sc;
     }
+    TWAIT();
+    TPROBE(5);
 }
 
 __global__ void __launch_bounds__(256)
@@ -243,7 +264,7 @@ inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / b
 
 hipError_t nv_run_launch(const NvParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
-    const size_t lds = (size_t)EPW * (p.L + 5) * sizeof(float);
+    const size_t lds = (size_t)((EPW * (p.L + 5) + 3) / 4) * 4 * sizeof(float) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
 #define L_(X)                                                                                       \
     do {                                                                                            \
@@ -286,3 +307,9 @@ hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, h
 }
 
 }  // namespace invsim
+
+#ifdef INVSIM_TIMING
+extern "C" int invsim_debug_timing_nv(void *dst, int64_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_tbuf), (size_t)bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -25,29 +25,37 @@ def main():
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--lostsales", action="store_true")
     ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--newsvendor", action="store_true")
     args = ap.parse_args()
     import invsim
     from invsim import _capi
-    cls = invsim.InvManagementLostSalesEnv if args.lostsales else invsim.InvManagementBacklogEnv
-    env = cls(num_envs=args.n)
-    env.reset(seed=0)
-    hi = torch.as_tensor(env.single_action_space.high, device=env.device)
-    g = torch.Generator(device=env.device).manual_seed(1)
-    acts = [torch.floor(torch.rand((args.n, env.action_dim), device=env.device, generator=g, dtype=torch.float64)
-                        * (hi + 1)).to(torch.int64) for _ in range(args.steps)]
+    g = torch.Generator(device="cuda").manual_seed(1)
+    if args.newsvendor:
+        env = invsim.NewsvendorEnv(num_envs=args.n)
+        env.reset(seed=0)
+        acts = [torch.rand((args.n, 1), device=env.device, generator=g) * 400 for _ in range(args.steps)]
+    else:
+        cls = invsim.InvManagementLostSalesEnv if args.lostsales else invsim.InvManagementBacklogEnv
+        env = cls(num_envs=args.n)
+        env.reset(seed=0)
+        hi = torch.as_tensor(env.single_action_space.high, device=env.device)
+        acts = [torch.floor(torch.rand((args.n, env.action_dim), device=env.device, generator=g,
+                                       dtype=torch.float64) * (hi + 1)).to(torch.int64) for _ in range(args.steps)]
     for a in acts:
         env.step(a)
     torch.cuda.synchronize()
     lib = _capi.lib()
     waves = min((args.n + 63) // 64, 4096)
     buf = np.zeros((4096, 8), dtype=np.uint64)
-    rc = lib.invsim_debug_timing(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
+    fn = lib.invsim_debug_timing_nv if args.newsvendor else lib.invsim_debug_timing
+    rc = fn(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
     assert rc == 0, rc
     b = buf[:waves].astype(np.int64)
     t0 = b[:, 0].min()
     ns = lambda x: (x * 10.0)
     print(f"waves {waves}; kernel span (first entry -> last exit) {ns(b[:, 5].max() - t0):.0f} ns")
-    names = ["entry", "loads issued", "demand", "dynamics+tile", "stores issued", "exit"]
+    names = (["entry", "pre-demand", "demand", "step+tile", "stores issued", "exit"] if args.newsvendor else
+             ["entry", "loads issued", "demand", "dynamics+tile", "stores issued", "exit"])
     print("phase               p0      p10     p50     p90     max   (ns)")
     print("entry offset     " + " ".join(f"{ns(v):7.0f}" for v in np.percentile(b[:, 0] - t0, [0, 10, 50, 90, 100])))
     for i in range(1, 6):
@@ -70,7 +78,7 @@ def main():
         m = xcc == x
         print(f"  xcc {x}: waves {m.sum():4d} entry [{ns(b[m,0].min()-t0):6.0f},{ns(b[m,0].max()-t0):6.0f}] "
               f"exit max {ns(b[m,5].max()-t0):6.0f}")
-    np.save(os.path.join(ROOT, "gpurun_out", f"timing_{'ls' if args.lostsales else 'bl'}_{args.n}.npy"), buf)
+    np.save(os.path.join(ROOT, "gpurun_out", f"timing_{'nv' if args.newsvendor else ('ls' if args.lostsales else 'bl')}_{args.n}.npy"), buf)
 
 
 if __name__ == "__main__":
