@@ -175,6 +175,45 @@ int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, 
  * applied).  Synchronous.  clear != 0 resets it. */
 int invsim_status(invsim_handle *h, uint32_t *flags, int32_t clear);
 
+/* ---- Closed-loop rollouts with an in-kernel heuristic agent.
+ * The reference's benchmark agents, restated on device:
+ *   INVSIM_POLICY_CONSTANT     ConstantOrderAgent  benchmark_NetInvMgmtBacklogEnv.py:119-135
+ *                              (any family: the same action every step)
+ *   INVSIM_POLICY_BASE_STOCK   BaseStockAgent      benchmark_InvManagementBacklogEnv.py:142-198
+ *                              (InvMgmt; also benchmark_InvManagementLostSalesEnv.py:137-165)
+ *   INVSIM_POLICY_ORDER_UP_TO  OrderUpToHeuristicAgent  benchmark_newsvendor.py:97-111 (Newsvendor)
+ * Per-env metrics (f64, accumulated with += so a caller may chain launches),
+ * the sums evaluate_agent keeps (benchmark_InvManagementBacklogEnv.py:346-440,
+ * benchmark_NetInvMgmtLostSalesEnv.py:241-312, benchmark_newsvendor.py:219-250):
+ *   [0] sum of rewards (TotalReward)   [1] steps
+ *   InvMgmt:    [2] demand_realized  [3] sales[0]  [4] unfulfilled[0]
+ *               [5] sum over stages of max(0, ending_inventory)
+ *   NetInvMgmt: [2] retail demand D  [3] retail sales S  [4] retail U[t+1]
+ *               [5 + j] X[t+1] of main node j (j < n_main)
+ *   Newsvendor: [0], [1] only
+ * Unavailable with SAME_STEP autoreset and (NetInvMgmt) for graphs other than
+ * the reference's default / custom ones (invsim_kernel_variant != 0). */
+#define INVSIM_POLICY_CONSTANT 1
+#define INVSIM_POLICY_BASE_STOCK 2
+#define INVSIM_POLICY_ORDER_UP_TO 3
+#define INVSIM_POLICY_MAX_ACTION 32
+
+typedef struct {
+    int32_t kind;            /* INVSIM_POLICY_* */
+    int32_t reserved;
+    double safety_factor;    /* BASE_STOCK / ORDER_UP_TO */
+    double mu;               /* BASE_STOCK: env.dist_param.get('mu', 10) as the agent reads it */
+    const void *constant;    /* CONSTANT: host array [action_dim] in the action dtype */
+} invsim_policy;
+
+int invsim_metrics_dim(const invsim_handle *h, int32_t *dim);
+
+/* K steps of every env under `policy`.  All outputs may be NULL: obs [K][N][O],
+ * reward / terminated / truncated [K][N], actions [K][N][A] (the actions the
+ * agent took), metrics [N][invsim_metrics_dim] (+=).  Autoreset as set. */
+int invsim_rollout_policy(invsim_handle *h, int32_t K, const invsim_policy *policy, void *obs, double *reward,
+                          uint8_t *terminated, uint8_t *truncated, void *actions, double *metrics, void *stream);
+
 /* Which kernel a handle runs: 0 = the generic kernel of its family, 1 / 2 =
  * NetInvMgmt specialised at compile time for the reference's default /
  * custom supply network (chosen at create when the graph equals one of them). */

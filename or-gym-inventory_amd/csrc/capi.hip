@@ -634,7 +634,8 @@ int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream)
 }
 
 static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, double *reward,
-                     uint8_t *terminated, uint8_t *truncated, void *final_obs, hipStream_t s) {
+                     uint8_t *terminated, uint8_t *truncated, void *final_obs, hipStream_t s,
+                     const PolicyIO *pol = nullptr) {
     int t_u = -1;
     if (h->t_known) {
         t_u = h->t_cur;
@@ -651,18 +652,19 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
     switch (h->family) {
         case INVSIM_NEWSVENDOR: {
             StepIO<float, float> io{K, (const float *)actions, (float *)obs, reward, terminated, truncated, (float *)final_obs};
-            e = nv_run_launch(h->nv, t_u, io, s);
+            e = nv_run_launch(h->nv, t_u, pol, io, s);
             break;
         }
         case INVSIM_INVMGMT: {
             StepIO<int64_t, int64_t> io{K, (const int64_t *)actions, (int64_t *)obs, reward, terminated, truncated,
                                         (int64_t *)final_obs};
-            e = im_run_launch(h->im, h->im_m1, h->im_backlog, t_u, io, s);
+            e = im_run_launch(h->im, h->im_m1, h->im_backlog, t_u, pol, io, s);
             break;
         }
         case INVSIM_NETINVMGMT: {
             StepIO<float, float> io{K, (const float *)actions, (float *)obs, reward, terminated, truncated, (float *)final_obs};
-            e = h->net_spec ? net_spec_launch(h->net_spec, h->net, t_u, io, s) : net_run_launch(h->net, t_u, io, s);
+            if (pol && !h->net_spec) return fail(h, INVSIM_EINVAL, "policy rollouts need the default or custom graph");
+            e = h->net_spec ? net_spec_launch(h->net_spec, h->net, t_u, pol, io, s) : net_run_launch(h->net, t_u, io, s);
             break;
         }
         default: return fail(h, INVSIM_EINVAL, "bad handle family");
@@ -694,6 +696,58 @@ int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, 
         return fail(h, INVSIM_EINVAL, "rollout does not return final_obs: use NEXT_STEP or DISABLED autoreset");
     DeviceGuard g(h->device);
     return run_steps(h, K, actions, obs, reward, terminated, truncated, nullptr, (hipStream_t)stream);
+}
+
+static int metrics_dim(const invsim_handle *h) {
+    switch (h->family) {
+        case INVSIM_NEWSVENDOR: return 2;
+        case INVSIM_INVMGMT: return 6;
+        case INVSIM_NETINVMGMT: return 5 + h->net.J;
+        default: return 0;
+    }
+}
+
+int invsim_metrics_dim(const invsim_handle *h, int32_t *dim) {
+    if (!h || !dim) return fail(nullptr, INVSIM_EINVAL, "null argument");
+    *dim = metrics_dim(h);
+    return INVSIM_OK;
+}
+
+int invsim_rollout_policy(invsim_handle *h, int32_t K, const invsim_policy *policy, void *obs, double *reward,
+                          uint8_t *terminated, uint8_t *truncated, void *actions, double *metrics, void *stream) {
+    if (!h || !policy) return fail(h, INVSIM_EINVAL, "null argument");
+    if (K < 0) return fail(h, INVSIM_EINVAL, "K must be >= 0");
+    if (K == 0) return INVSIM_OK;
+    if (h->cm.autoreset == AR_SAME_STEP)
+        return fail(h, INVSIM_EINVAL, "policy rollouts do not return final_obs: use NEXT_STEP or DISABLED autoreset");
+    if ((reward == nullptr) != (terminated == nullptr) || (reward == nullptr) != (truncated == nullptr))
+        return fail(h, INVSIM_EINVAL, "reward, terminated and truncated are given together or not at all");
+    PolicyIO p{};
+    p.kind = policy->kind;
+    p.sf = policy->safety_factor;
+    p.mu = policy->mu;
+    p.act_out = actions;
+    p.metrics = metrics;
+    p.mdim = metrics_dim(h);
+    switch (policy->kind) {
+        case INVSIM_POLICY_CONSTANT:
+            if (!policy->constant) return fail(h, INVSIM_EINVAL, "CONSTANT policy needs its action vector");
+            if (h->act_dim > POL_MAX_A) return fail(h, INVSIM_ERANGE, "action_dim too large for a CONSTANT policy");
+            for (int a = 0; a < h->act_dim; a++) {
+                if (h->family == INVSIM_INVMGMT) p.ci[a] = ((const int64_t *)policy->constant)[a];
+                else p.cf[a] = ((const float *)policy->constant)[a];
+            }
+            break;
+        case INVSIM_POLICY_BASE_STOCK:
+            if (h->family != INVSIM_INVMGMT) return fail(h, INVSIM_EINVAL, "BASE_STOCK is an InvMgmt policy");
+            break;
+        case INVSIM_POLICY_ORDER_UP_TO:
+            if (h->family != INVSIM_NEWSVENDOR) return fail(h, INVSIM_EINVAL, "ORDER_UP_TO is a Newsvendor policy");
+            break;
+        default: return fail(h, INVSIM_EINVAL, "unknown policy kind");
+    }
+    DeviceGuard g(h->device);
+    return run_steps(h, K, nullptr, obs, reward, terminated, truncated, nullptr, (hipStream_t)stream, &p);
 }
 
 int invsim_kernel_variant(const invsim_handle *h, int32_t *variant) {

@@ -77,7 +77,7 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
                                              ImState<M1, BACKLOG> &s,
                                              const int64_t *__restrict__ arow, int64_t *orow,
                                              const double *rhs, TableStage *ts, double apow, int64_t udem,
-                                             double &reward, int64_t &dem_out) {
+                                             double &reward, int64_t &dem_out, double *met) {
     const int64_t S = P.cm.Npad;
     const int D = P.lt_max;
     const bool leader = valid && j == 0;   // state writes
@@ -178,6 +178,15 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
 #pragma unroll
     for (int q = 0; q <= M1; q++) s.B[q] = BACKLOG ? U[q] : 0;      // :307-312
     dem_out = d;
+    if (met) {   // evaluate_agent metrics (benchmark_InvManagementBacklogEnv.py:378-399)
+        met[2] += (double)d;                                        // demand_realized
+        met[3] += (double)Sv[0];                                    // sales[0]
+        met[4] += (double)U[0];                                     // unfulfilled[0]
+        int64_t es = 0;                                             // sum(max(0, ending_inventory))
+#pragma unroll
+        for (int i = 0; i < M1; i++) es = wrap_add(es, Icur[i] > 0 ? Icur[i] : 0);
+        met[5] += (double)es;
+    }
     if (orow) {                                                     // :354-391
         int64_t *w = orow + M1;
         if (j == 0) {
@@ -212,14 +221,46 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
     return t1 >= P.periods;                                         // :350
 }
 
+// BaseStockAgent.get_action (benchmark_InvManagementBacklogEnv.py:152-198): order
+// up to (L_i + 1) * mu * sf over the inventory position on hand + requested
+// orders of the last L_i periods (action_log[max(0, t - L_i) : t, i]), in
+// float64, clipped to [0, c_i], truncated to int64.
+template <int M1, bool BACKLOG>
+__device__ __forceinline__ void im_base_stock(const ImParams &P, const PolicyIO &pol, const ImState<M1, BACKLOG> &st,
+                                              int t, int64_t e, int64_t (&act)[M1]) {
+    const int64_t S = P.cm.Npad;
+    const int D = P.lt_max;
+#pragma unroll
+    for (int i = 0; i < M1; i++) {
+        const int L = P.L[i];
+        int64_t pos = st.I[i];                                      // observation[:M1] = I[t]
+        if (L > 0) {
+            int64_t pipe = 0;
+            for (int a = 1; a <= L; a++) {
+                const int tau = t - a;
+                if (tau >= 0)
+                    pipe = wrap_add(pipe, P.alog[((int64_t)((uint32_t)tau % (uint32_t)D) * M1 + i) * S + e]);
+            }
+            pos = wrap_add(pos, pipe);
+        }
+        const double target = ((double)(L + 1) * pol.mu) * pol.sf;   // (lead_times + 1) * mu * sf
+        double x = target - (double)pos;
+        x = (x > 0) ? x : 0.0;                                      // np.maximum(0, .)
+        x = (x < 0.0) ? 0.0 : x;                                    // np.clip(., low = 0, high = c)
+        x = (x > (double)P.c[i]) ? (double)P.c[i] : x;
+        act[i] = (int64_t)x;                                        // astype(int64)
+    }
+}
+
 // Step k of a launch for the wave's envs: step (or NEXT_STEP reset) into the
 // LDS obs tile, SAME_STEP final-obs/reset, then the tile's coalesced store.
-template <int M1, bool BACKLOG, bool STEP_ONLY>
+template <int M1, bool BACKLOG, bool STEP_ONLY, bool POL>
 __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<int64_t, int64_t> &io, int k,
                                                int64_t e, int64_t e0, int lane, bool valid, int nvalid,
                                                ImState<M1, BACKLOG> &st, int &t, bool &fault,
                                                int64_t *tile, int64_t *trow, const double *rhs,
-                                               TableStage *ts, const double *pre_apow, const int64_t *pre_udem) {
+                                               TableStage *ts, const double *pre_apow, const int64_t *pre_udem,
+                                               const PolicyIO &pol, double *met) {
     const int j = lane & (LPE - 1);
     const bool leader = j == 0;
     const int64_t N = P.cm.N;
@@ -233,7 +274,7 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
     if (!STEP_ONLY && t >= P.periods) {
         if (P.cm.autoreset == AR_NEXT_STEP) {
             im_reset_regs<M1, BACKLOG>(P, st, trow, j);
-            if (valid && leader) {
+            if (valid && leader && (!POL || io.rew)) {
                 out_store(io.rew + oi, 0.0);
                 out_store(io.term + oi, (uint8_t)0);
                 out_store(io.trunc + oi, (uint8_t)0);
@@ -252,13 +293,33 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
         // before any store of the step (vmcnt counts stores too) unless preloaded
         const double apow = pre_apow ? *pre_apow : P.alpha_pow[t];
         const int64_t udem = pre_udem ? *pre_udem : P.user_D[t];
-        tr = im_step_regs<M1, BACKLOG>(P, e, valid, j, t, st, io.act + ea * M1, trow, rhs, ts, apow, udem, r, d);
-        if (valid && leader) {
+        const int64_t *arow = io.act + ea * M1;
+        int64_t pact[M1];
+        if (POL) {
+            if (pol.kind == POL_BASE_STOCK) {
+                im_base_stock<M1, BACKLOG>(P, pol, st, t, e, pact);
+            } else {
+#pragma unroll
+                for (int i = 0; i < M1; i++) pact[i] = pol.ci[i];
+            }
+            if (valid && pol.act_out) {
+#pragma unroll
+                for (int i = 0; i < M1; i++) out_store((int64_t *)pol.act_out + oi * M1 + i, pact[i]);
+            }
+            arow = pact;
+        }
+        tr = im_step_regs<M1, BACKLOG>(P, e, valid, j, t, st, arow, trow, rhs, ts, apow, udem, r, d,
+                                       POL ? met : nullptr);
+        if (POL) {
+            met[0] += r;                                            // episode_reward += reward
+            met[1] += 1.0;                                          // episode_steps
+        }
+        if (valid && leader && (!POL || io.rew)) {
             out_store(io.rew + oi, r);
             out_store(io.term + oi, (uint8_t)0);
             out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
-            if (k == io.K - 1 && P.cm.info_demand) P.cm.info_demand[e] = d;
         }
+        if (valid && leader && k == io.K - 1 && P.cm.info_demand) P.cm.info_demand[e] = d;
         t += 1;
     }
     wave_lds_sync();
@@ -274,16 +335,17 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
     }
 #ifndef INVSIM_ABL_NO_OBS  // profiling ablation build only
     // obs tile: at most 64 * M1 * 11 int64 in register-window configurations
-    store_tile<(M1 * 11 * EPW * 8 + 16 * WAVE - 1) / (16 * WAVE)>(tile, io.obs + ((int64_t)k * N + e0) * O,
-                                                                 (int64_t)nvalid * O, lane);
+    if (!POL || io.obs)
+        store_tile<(M1 * 11 * EPW * 8 + 16 * WAVE - 1) / (16 * WAVE)>(tile, io.obs + ((int64_t)k * N + e0) * O,
+                                                                     (int64_t)nvalid * O, lane);
 #endif
     TPROBE(4);
     wave_lds_sync();
 }
 
-template <int M1, bool BACKLOG, bool TU, bool ONE>
+template <int M1, bool BACKLOG, bool TU, bool ONE, bool POL>
 __global__ void __launch_bounds__(WAVE)
-im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io) {
+im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
     const int lane = threadIdx.x;
     const int j = lane & (LPE - 1);
@@ -349,14 +411,18 @@ im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io) {
     for (int q = 0; q <= M1; q++) st.B[q] = BACKLOG ? P.B[q * S + e] : 0;
     int t = t0;
     bool fault = false;
+    constexpr int MD = 6;                       // metrics (invsim.h INVSIM_METRICS_*)
+    double met[MD];
+#pragma unroll
+    for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[(valid ? e : N - 1) * MD + q] : 0.0;
     if (ONE) {
-        im_launch_step<M1, BACKLOG, TU>(P, io, 0, e, e0, lane, valid, nvalid, st, t, fault, im_tile, trow, rhs_l,
-                                        &ts, &apow0, &udem0);
+        im_launch_step<M1, BACKLOG, TU, false>(P, io, 0, e, e0, lane, valid, nvalid, st, t, fault, im_tile, trow,
+                                               rhs_l, &ts, &apow0, &udem0, pol, met);
     } else {
         ts.flush(lane);
         for (int k = 0; k < io.K; k++)
-            im_launch_step<M1, BACKLOG, false>(P, io, k, e, e0, lane, valid, nvalid, st, t, fault, im_tile, trow,
-                                               rhs_l, nullptr, nullptr, nullptr);
+            im_launch_step<M1, BACKLOG, false, POL>(P, io, k, e, e0, lane, valid, nvalid, st, t, fault, im_tile,
+                                                    trow, rhs_l, nullptr, nullptr, nullptr, pol, met);
     }
     if (valid && leader) {
         P.cm.rng.store_state(e, st.g);
@@ -368,6 +434,10 @@ im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io) {
         }
         if (!TU) P.cm.period[e] = t;
         if (fault) atomicOr(P.cm.status, 1u);
+        if (POL && pol.metrics) {
+#pragma unroll
+            for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
+        }
     }
     TWAIT();
     TPROBE(5);
@@ -411,27 +481,31 @@ inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / b
         default: return hipErrorInvalidValue;                          \
     }
 
-hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u,
+hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
                          const StepIO<int64_t, int64_t> &io, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = (size_t)EPW * M1 * (p.lt_max + 1) * sizeof(int64_t) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
-#define L_(M, B)                                                                                      \
-    do {                                                                                              \
-        if (io.K == 1) {                                                                              \
-            if (t_u >= 0)                                                                             \
-                hipLaunchKernelGGL((im_run_kernel<M, B, true, true>), grid, block, lds, s, p, t_u, io);  \
-            else                                                                                      \
-                hipLaunchKernelGGL((im_run_kernel<M, B, false, true>), grid, block, lds, s, p, t_u, io); \
-        } else {                                                                                      \
-            if (t_u >= 0)                                                                             \
-                hipLaunchKernelGGL((im_run_kernel<M, B, true, false>), grid, block, lds, s, p, t_u, io); \
-            else                                                                                      \
-                hipLaunchKernelGGL((im_run_kernel<M, B, false, false>), grid, block, lds, s, p, t_u, io);\
-        }                                                                                             \
+    PolicyIO none{};
+    const PolicyIO &pv = pol ? *pol : none;
+#define K_(M, B, TU, ONE, POL) \
+    hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
+#define L_(M, B)                                             \
+    do {                                                     \
+        if (pol) {                                           \
+            if (t_u >= 0) K_(M, B, true, false, true);       \
+            else K_(M, B, false, false, true);               \
+        } else if (io.K == 1) {                              \
+            if (t_u >= 0) K_(M, B, true, true, false);       \
+            else K_(M, B, false, true, false);               \
+        } else {                                             \
+            if (t_u >= 0) K_(M, B, true, false, false);      \
+            else K_(M, B, false, false, false);              \
+        }                                                    \
     } while (0)
     IM_DISPATCH(M1, backlog, L_)
 #undef L_
+#undef K_
     return hipGetLastError();
 }
 

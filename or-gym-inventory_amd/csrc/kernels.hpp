@@ -119,6 +119,21 @@ struct StepIO {
     O *fobs;           // [N][obs_dim] final obs (SAME_STEP, K == 1), may be null
 };
 
+// Closed-loop rollouts (invsim_rollout_policy): each step's action is computed
+// in the kernel from the env state by a restated heuristic agent, every output
+// is optional, and per-env evaluation metrics accumulate in registers.
+enum { POL_NONE = 0, POL_CONSTANT = 1, POL_BASE_STOCK = 2, POL_ORDER_UP_TO = 3 };
+constexpr int POL_MAX_A = 32;
+struct PolicyIO {
+    int32_t kind;
+    int32_t mdim;             // metrics per env (0: none)
+    double sf, mu;            // safety factor; BASE_STOCK demand mean
+    int64_t ci[POL_MAX_A];    // CONSTANT actions, int64 action spaces
+    float cf[POL_MAX_A];      // CONSTANT actions, f32 action spaces
+    void *act_out;            // [K][N][action_dim] actions taken, may be null
+    double *metrics;          // [N][mdim], accumulated (+=), may be null
+};
+
 // Lock-step period: when every env of the handle is at the same period the host
 // knows it (t_u >= 0) and the kernels neither read nor write the per-env
 // period row; t_u = -1 means "read period[e]".  Next period after one step at t
@@ -250,17 +265,19 @@ hipError_t seed_words_launch(const Common &cm, const uint32_t *words, const int3
 hipError_t period_fill_launch(const Common &cm, int32_t t, hipStream_t s);
 
 hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, hipStream_t s);
-hipError_t nv_run_launch(const NvParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s);
+hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
+                         hipStream_t s);
 
 hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_t *mask,
                            int64_t *obs, hipStream_t s);
-hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u,
+hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
                          const StepIO<int64_t, int64_t> &io, hipStream_t s);
 
 // Compile-time specialised NetInvMgmt kernels for the reference's own graphs
 // (netspec.hip): which built-in topology a spec equals, and its launcher.
 enum { NET_SPEC_NONE = 0, NET_SPEC_DEFAULT = 1, NET_SPEC_CUSTOM = 2 };
-hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s);
+hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const PolicyIO *pol,
+                           const StepIO<float, float> &io, hipStream_t s);
 hipError_t net_reset_launch(const NetParams &p, const uint8_t *mask, float *obs, hipStream_t s);
 hipError_t net_run_launch(const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s);
 size_t net_lds_bytes(const NetParams &p);

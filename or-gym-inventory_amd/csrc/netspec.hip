@@ -61,7 +61,8 @@ __device__ __forceinline__ void spec_reset(NetSt<G> &s, float *orow) {
 template <class G>
 __device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst (&pc)[G::RL], const double *rhs_l,
                                             int t, double apow, NetSt<G> &s, const float (&act)[G::E],
-                                            float *orow, double (&Rn)[G::E], int64_t (&dem)[G::RL]) {
+                                            float *orow, double (&Rn)[G::E], int64_t (&dem)[G::RL],
+                                            double *met) {
     // market demand draws, retail-link order (:536-541)
     double Dd[G::RL];
 #pragma unroll
@@ -121,6 +122,16 @@ __device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst 
         s.X[node] -= sale;
         Sr[r] = sale;
         s.U[r] = P.backlog ? fill - sale : 0.0;
+    }
+    if (met) {   // evaluate_agent metrics (benchmark_NetInvMgmtLostSalesEnv.py:264-300)
+#pragma unroll
+        for (int r = 0; r < G::RL; r++) {
+            met[2] += Dd[r];                  // D[t, retail links]
+            met[3] += Sr[r];                  // S[t, retail links]
+            met[4] += s.U[r];                 // U[t+1, retail links]
+        }
+#pragma unroll
+        for (int j = 0; j < G::J; j++) met[5 + j] += s.X[j];   // X[t+1, main nodes] per node
     }
     // 5) profit per main node (:578-613), Python sum() order = adjacency order
     double total = 0.0;
@@ -183,9 +194,9 @@ __device__ __forceinline__ void spec_shift(NetSt<G> &s, const double (&Rn)[G::E]
     }
 }
 
-template <class G, bool TU, bool ONE>
+template <class G, bool TU, bool ONE, bool POL>
 __global__ void __launch_bounds__(WAVE)
-net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io) {
+net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) float ns_lds[];
     constexpr int O = G::O;
     constexpr int TILE_IT = (EPW * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
@@ -256,7 +267,11 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io) {
     }
     float act[G::E];
 #pragma unroll
-    for (int k = 0; k < G::E; k++) act[k] = io.act[el * G::E + k];
+    for (int k = 0; k < G::E; k++) act[k] = POL ? pol.cf[k] : io.act[el * G::E + k];
+    constexpr int MD = 5 + G::J;             // metrics: reward, steps, demand, sales, stockout, X per node
+    double met[MD];
+#pragma unroll
+    for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
 #pragma unroll
     for (int r = 0; r < G::RL; r++)
 #pragma unroll
@@ -274,8 +289,10 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io) {
         const int64_t oi = (int64_t)kk * N + e;
         if (kk > 0) {
             const int64_t ea = (int64_t)kk * N + el;
+            if (!POL) {
 #pragma unroll
-            for (int k = 0; k < G::E; k++) act[k] = io.act[ea * G::E + k];
+                for (int k = 0; k < G::E; k++) act[k] = io.act[ea * G::E + k];
+            }
             apow = P.alpha_pow[(t < P.T) ? t : 0];
         }
         bool tr = false;
@@ -283,7 +300,7 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io) {
             if (P.cm.autoreset == AR_NEXT_STEP) {
                 spec_reset<G>(st, trow);
                 dirty_all = true;
-                if (valid) {
+                if (valid && (!POL || io.rew)) {
                     out_store(io.rew + oi, 0.0);
                     out_store(io.term + oi, (uint8_t)0);
                     out_store(io.trunc + oi, (uint8_t)0);
@@ -294,12 +311,22 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io) {
             }
         } else {
             int64_t dem[G::RL];
-            const double r = spec_step<G>(P, pc, rhs_l, t, apow, st, act, trow, Rn, dem);
+            const double r = spec_step<G>(P, pc, rhs_l, t, apow, st, act, trow, Rn, dem, POL ? met : nullptr);
             tr = t + 1 >= P.T;
-            if (valid) {
+            if (POL) {
+                met[0] += r;                    // episode_reward += reward
+                met[1] += 1.0;
+                if (valid && pol.act_out) {
+#pragma unroll
+                    for (int k = 0; k < G::E; k++) out_store((float *)pol.act_out + oi * G::E + k, act[k]);
+                }
+            }
+            if (valid && (!POL || io.rew)) {
                 out_store(io.rew + oi, r);
                 out_store(io.term + oi, (uint8_t)0);
                 out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
+            }
+            if (valid) {
                 if (kk == K - 1 && P.cm.info_demand) {
 #pragma unroll
                     for (int q = 0; q < G::RL; q++) P.cm.info_demand[e * G::RL + q] = dem[q];
@@ -330,7 +357,7 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io) {
             t = 0;
         }
         wave_lds_sync();
-        store_tile<TILE_IT>(tile, io.obs + ((int64_t)kk * N + e0) * O, (int64_t)nvalid * O, lane);
+        if (!POL || io.obs) store_tile<TILE_IT>(tile, io.obs + ((int64_t)kk * N + e0) * O, (int64_t)nvalid * O, lane);
         wave_lds_sync();
     }
     if (valid) {
@@ -355,6 +382,10 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io) {
         }
         if (!TU) P.cm.period[e] = t;
         if (fault) atomicOr(P.cm.status, 1u);
+        if (POL && pol.metrics) {
+#pragma unroll
+            for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
+        }
     }
     (void)t_start;
 }
@@ -397,28 +428,33 @@ static size_t spec_lds_bytes() {
 }
 
 template <class G>
-static hipError_t spec_launch(const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s) {
+static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
+                              hipStream_t s) {
     const size_t lds = spec_lds_bytes<G>();
     const dim3 grid((unsigned)((p.cm.N + EPW - 1) / EPW)), block(WAVE);
-    if (io.K == 1) {
-        if (t_u >= 0)
-            hipLaunchKernelGGL((net_spec_kernel<G, true, true>), grid, block, lds, s, p, t_u, io);
-        else
-            hipLaunchKernelGGL((net_spec_kernel<G, false, true>), grid, block, lds, s, p, t_u, io);
+    PolicyIO none{};
+    const PolicyIO &pv = pol ? *pol : none;
+#define K_(TU, ONE, POL) hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
+    if (pol) {
+        if (t_u >= 0) K_(true, false, true);
+        else K_(false, false, true);
+    } else if (io.K == 1) {
+        if (t_u >= 0) K_(true, true, false);
+        else K_(false, true, false);
     } else {
-        if (t_u >= 0)
-            hipLaunchKernelGGL((net_spec_kernel<G, true, false>), grid, block, lds, s, p, t_u, io);
-        else
-            hipLaunchKernelGGL((net_spec_kernel<G, false, false>), grid, block, lds, s, p, t_u, io);
+        if (t_u >= 0) K_(true, false, false);
+        else K_(false, false, false);
     }
+#undef K_
     return hipGetLastError();
 }
 
-hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s) {
+hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const PolicyIO *pol,
+                           const StepIO<float, float> &io, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     switch (which) {
-        case NET_SPEC_DEFAULT: return spec_launch<NetTopoDefault>(p, t_u, io, s);
-        case NET_SPEC_CUSTOM: return spec_launch<NetTopoCustom>(p, t_u, io, s);
+        case NET_SPEC_DEFAULT: return spec_launch<NetTopoDefault>(p, t_u, pol, io, s);
+        case NET_SPEC_CUSTOM: return spec_launch<NetTopoCustom>(p, t_u, pol, io, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -89,6 +89,37 @@ __device__ __forceinline__ void nv_reset_regs(const NvParams &P, int64_t e, NvSt
     }
 }
 
+// Sum of the pipeline as the observation holds it (float32, numpy pairwise
+// order): observation[5:].sum()
+template <int LT>
+__device__ __forceinline__ float nv_pipe_sum(const NvParams &P, int64_t e, int sc, const NvState<LT> &s) {
+    const int64_t S = P.cm.Npad;
+    const int L = (LT >= 0) ? LT : P.L;
+    const int base = (L > 0) ? (int)((uint32_t)(sc + 1) % (uint32_t)L) : 0;
+    return np_sum<float>(L, [&](int p) -> float {
+        if (LT > 0) return s.pv[p];
+        int sl = base + p;
+        sl = sl >= L ? sl - L : sl;
+        return (p >= L - sc) ? P.pipe[(int64_t)sl * S + e] : 0.f;
+    });
+}
+
+// OrderUpToHeuristicAgent.get_action (benchmark_newsvendor.py:103-111), float32
+// as numpy evaluates it: target = mu * (L + 1) * sf, order max(0, target -
+// pipeline.sum()) clipped to the action space [0, max_order_quantity]
+template <int LT>
+__device__ __forceinline__ float nv_order_up_to(const NvParams &P, const PolicyIO &pol, int64_t e, int sc,
+                                                const NvState<LT> &s) {
+    const int L = (LT >= 0) ? LT : P.L;
+    const float mu = (float)s.par[4];                                  // observation[4]
+    const float target = (mu * (float)(L + 1)) * (float)pol.sf;
+    const float q = target - nv_pipe_sum<LT>(P, e, sc, s);
+    float o = (q > 0.f) ? q : 0.f;                                      // builtin max(0, q)
+    const float hi = (float)P.max_order;
+    o = (o < 0.f) ? 0.f : o;                                            // np.clip(., low[0], high[0])
+    return (o > hi) ? hi : o;
+}
+
 // One newsvendor.py:125-204 step at step count sc.  Returns truncated.
 template <int LT>
 __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool valid, int sc, NvState<LT> &s,
@@ -143,9 +174,9 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
     return sc + 1 >= P.step_limit;                                          // :190
 }
 
-template <int LT, bool TU, bool ONE>
+template <int LT, bool TU, bool ONE, bool POL>
 __global__ void __launch_bounds__(WAVE)
-nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
+nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) float nv_tile[];
     const int lane = threadIdx.x;
     const bool leader = (lane & (LPE - 1)) == 0;
@@ -199,16 +230,21 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
             if (!(p >= LT - sc)) st.pv[p] = 0.f;
         }
     }
+    constexpr int MD = 2;                       // metrics: reward sum, steps
+    double met[MD];
+#pragma unroll
+    for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
     const int K = ONE ? 1 : io.K;
     // all lanes write the table: before any divergent step/reset branch (with a
     // lock-step single step there is none, and the write waits inside the step)
     if (!(ONE && TU)) ts.flush(lane);
     for (int k = 0; k < K; k++) {
         const int64_t oi = (int64_t)k * N + e;
-        const float act = io.act[(int64_t)k * N + el];
+        float act;
+        if (!POL) act = io.act[(int64_t)k * N + el];
         if (!(ONE && TU) && P.cm.autoreset == AR_NEXT_STEP && sc >= P.step_limit) {
             nv_reset_regs<LT>(P, e, st, trow, valid);
-            if (valid) {
+            if (valid && (!POL || io.rew)) {
                 out_store(io.rew + oi, 0.0);
                 out_store(io.term + oi, (uint8_t)0);
                 out_store(io.trunc + oi, (uint8_t)0);
@@ -216,9 +252,17 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
             sc = 0;
         } else {
             double r;
+            if (POL) {
+                act = (pol.kind == POL_ORDER_UP_TO) ? nv_order_up_to<LT>(P, pol, e, sc, st) : pol.cf[0];
+                if (valid && pol.act_out) out_store((float *)pol.act_out + oi, act);
+            }
             const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, ts.dst, (ONE && TU) ? &ts : nullptr, r,
                                              (valid && k == K - 1) ? P.cm.info_demand : nullptr);
-            if (valid) {
+            if (POL) {
+                met[0] += r;                    // episode_reward += reward (benchmark_newsvendor.py:241)
+                met[1] += 1.0;
+            }
+            if (valid && (!POL || io.rew)) {
                 out_store(io.rew + oi, r);
                 out_store(io.term + oi, (uint8_t)0);
                 out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
@@ -234,13 +278,17 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io) {
             }
         }
         wave_lds_sync();
-        store_tile<TILE_IT>(nv_tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+        if (!POL || io.obs) store_tile<TILE_IT>(nv_tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
         TPROBE(4);
         wave_lds_sync();
     }
     if (valid) {
         P.cm.rng.store_state(e, st.g);
         if (!TU) P.cm.period[e] = sc;
+        if (POL && pol.metrics) {
+#pragma unroll
+            for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
+        }
     }
     TWAIT();
     TPROBE(5);
@@ -262,23 +310,27 @@ inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / b
 
 }  // namespace
 
-hipError_t nv_run_launch(const NvParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s) {
+hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
+                         hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = (size_t)((EPW * (p.L + 5) + 3) / 4) * 4 * sizeof(float) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
-#define L_(X)                                                                                       \
-    do {                                                                                            \
-        if (io.K == 1) {                                                                            \
-            if (t_u >= 0)                                                                           \
-                hipLaunchKernelGGL((nv_run_kernel<X, true, true>), grid, block, lds, s, p, t_u, io);  \
-            else                                                                                    \
-                hipLaunchKernelGGL((nv_run_kernel<X, false, true>), grid, block, lds, s, p, t_u, io); \
-        } else {                                                                                    \
-            if (t_u >= 0)                                                                           \
-                hipLaunchKernelGGL((nv_run_kernel<X, true, false>), grid, block, lds, s, p, t_u, io); \
-            else                                                                                    \
-                hipLaunchKernelGGL((nv_run_kernel<X, false, false>), grid, block, lds, s, p, t_u, io);\
-        }                                                                                           \
+    PolicyIO none{};
+    const PolicyIO &pv = pol ? *pol : none;
+#define K_(X, TU, ONE, POL) \
+    hipLaunchKernelGGL((nv_run_kernel<X, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
+#define L_(X)                                          \
+    do {                                               \
+        if (pol) {                                     \
+            if (t_u >= 0) K_(X, true, false, true);    \
+            else K_(X, false, false, true);            \
+        } else if (io.K == 1) {                        \
+            if (t_u >= 0) K_(X, true, true, false);    \
+            else K_(X, false, true, false);            \
+        } else {                                       \
+            if (t_u >= 0) K_(X, true, false, false);   \
+            else K_(X, false, false, false);           \
+        }                                              \
     } while (0)
     switch (p.L) {
         case 0: L_(0); break;
@@ -297,6 +349,7 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const StepIO<float, float> 
         default: L_(-1); break;
     }
 #undef L_
+#undef K_
     return hipGetLastError();
 }
 

@@ -21,13 +21,24 @@ _LAZY = {
     "NetInvMgmtMasterEnv": "network_management",
     "NetInvMgmtBacklogEnv": "network_management",
     "NetInvMgmtLostSalesEnv": "network_management",
+    "BaseStockAgent": "policies",
+    "ConstantOrderAgent": "policies",
+    "OrderUpToHeuristicAgent": "policies",
+    "evaluate_agent": "policies",
+    "rollout_policy": "policies",
 }
 
 
+_SUBMODULES = ("policies", "topology", "distributed", "spaces", "vector", "newsvendor",
+               "inventory_management", "network_management")
+
+
 def __getattr__(name):
+    import importlib
     if name in _LAZY:
-        import importlib
         return getattr(importlib.import_module(f".{_LAZY[name]}", __name__), name)
+    if name in _SUBMODULES:
+        return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)
 
 

@@ -22,7 +22,8 @@ EXPORTS = (
     "invsim_abi_version", "invsim_last_error", "invsim_create_newsvendor",
     "invsim_create_invmgmt", "invsim_create_netinvmgmt", "invsim_destroy", "invsim_dims",
     "invsim_set_autoreset", "invsim_seed_range", "invsim_seed_words", "invsim_reset",
-    "invsim_step", "invsim_rollout", "invsim_status", "invsim_kernel_variant", "invsim_set_info_demand",
+    "invsim_step", "invsim_rollout", "invsim_status", "invsim_kernel_variant", "invsim_metrics_dim",
+    "invsim_rollout_policy", "invsim_set_info_demand",
     "invsim_state_bytes",
     "invsim_state_field", "invsim_get_state", "invsim_set_state",
 )
@@ -54,6 +55,14 @@ class NetInvMgmtSpec(C.Structure):
         (n, C.c_void_p) for n in NET_TABLE_FIELDS]
 
 
+POLICY_KINDS = {"constant": 1, "base_stock": 2, "order_up_to": 3}
+
+
+class PolicySpec(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32), ("safety_factor", C.c_double),
+                ("mu", C.c_double), ("constant", C.c_void_p)]
+
+
 class InvsimError(RuntimeError):
     pass
 
@@ -80,6 +89,8 @@ def _declare(lib):
         "invsim_rollout": ([H, I32, P, P, P, P, P, P], C.c_int),
         "invsim_status": ([H, P, I32], C.c_int),
         "invsim_kernel_variant": ([H, P], C.c_int),
+        "invsim_metrics_dim": ([H, P], C.c_int),
+        "invsim_rollout_policy": ([H, I32, P, P, P, P, P, P, P, P], C.c_int),
         "invsim_set_info_demand": ([H, P], C.c_int),
         "invsim_state_bytes": ([H, P], C.c_int),
         "invsim_state_field": ([H, I32, P, P, P, P, P], C.c_int),

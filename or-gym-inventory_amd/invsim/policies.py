@@ -1,0 +1,158 @@
+"""Device-side heuristic agents and batched ``evaluate_agent``.
+
+The reference's benchmark scripts drive one env per episode from Python:
+``agent.get_action(obs, env)`` then ``env.step``, accumulating per-episode sums
+(``evaluate_agent``).  Here the agent runs inside the step kernel
+(``invsim_rollout_policy``): N episodes advance together with no host round
+trip, and the per-env sums come back as one array.
+
+Agents (restated from the reference, same names and constructor arguments):
+
+* ``BaseStockAgent(safety_factor)``        benchmark_InvManagementBacklogEnv.py:142-198
+  (and benchmark_InvManagementLostSalesEnv.py:137-165), InvMgmt envs
+* ``ConstantOrderAgent(order_fraction)``   benchmark_NetInvMgmtBacklogEnv.py:119-135
+  (and benchmark_NetInvMgmtLostSalesEnv.py:131-142), any env
+* ``OrderUpToHeuristicAgent(safety_factor)`` benchmark_newsvendor.py:97-111, Newsvendor
+
+``evaluate_agent(agent, env_cls, env_config, n_episodes, seed_offset)`` returns
+the reference's summary columns (benchmark_InvManagementBacklogEnv.py:346-440,
+benchmark_NetInvMgmtLostSalesEnv.py:241-312, benchmark_newsvendor.py:219-262):
+episode i is env i seeded ``seed_offset + i``.
+"""
+import ctypes as C
+import time
+
+import numpy as np
+import torch
+
+from . import _capi
+
+
+class _Agent:
+    kind = None
+    name = "agent"
+
+    def device_spec(self, env):
+        """(PolicySpec, keep-alive) for invsim_rollout_policy."""
+        raise NotImplementedError
+
+
+class BaseStockAgent(_Agent):
+    """Independent base-stock level (L_i + 1) * mu * safety_factor per stage."""
+
+    def __init__(self, safety_factor=1.0):
+        self.name = f"BaseStock_SF={safety_factor:.1f}"
+        self.safety_factor = safety_factor
+
+    def device_spec(self, env):
+        if env.family != _capi.INVSIM_INVMGMT:
+            raise TypeError("BaseStockAgent needs an InvManagement env")
+        mu = env.dist_param.get("mu", 10)       # the agent's own default (:156)
+        return _capi.PolicySpec(_capi.POLICY_KINDS["base_stock"], 0, float(self.safety_factor), float(mu), None), None
+
+
+class ConstantOrderAgent(_Agent):
+    """order_fraction * action_space.high every step (inf bounds -> 1000)."""
+
+    def __init__(self, order_fraction=0.1):
+        self.name = f"ConstantOrder_{order_fraction * 100:.0f}%"
+        self.order_fraction = order_fraction
+
+    def action(self, env):
+        sp = env.single_action_space
+        high = np.array(sp.high, copy=True)
+        high[high == np.inf] = 1000
+        return (high * self.order_fraction).astype(sp.dtype)
+
+    def device_spec(self, env):
+        a = np.ascontiguousarray(self.action(env))
+        return _capi.PolicySpec(_capi.POLICY_KINDS["constant"], 0, 0.0, 0.0, a.ctypes.data), a
+
+
+class OrderUpToHeuristicAgent(_Agent):
+    """Order up to mu * (lead_time + 1) * safety_factor over the pipeline."""
+
+    def __init__(self, safety_factor=1.0):
+        self.name = f"OrderUpTo_SF={safety_factor:.1f}"
+        self.safety_factor = safety_factor
+
+    def device_spec(self, env):
+        if env.family != _capi.INVSIM_NEWSVENDOR:
+            raise TypeError("OrderUpToHeuristicAgent needs a Newsvendor env")
+        return _capi.PolicySpec(_capi.POLICY_KINDS["order_up_to"], 0, float(self.safety_factor), 0.0, None), None
+
+
+def rollout_policy(env, agent, K, obs=False, rewards=True, actions=False, metrics=None):
+    """K steps of every env of ``env`` under ``agent`` (in-kernel).  Returns a
+    dict with the requested device tensors; ``metrics`` (float64 [N, M]) is
+    accumulated in place when given."""
+    spec, keep = agent.device_spec(env)
+    N, dev = env.num_envs, env.device
+    out = {}
+    o = torch.empty((K, N, env.obs_dim), dtype=env.obs_dtype, device=dev) if obs else None
+    if rewards:
+        out["reward"] = torch.empty((K, N), dtype=torch.float64, device=dev)
+        out["terminated"] = torch.empty((K, N), dtype=torch.bool, device=dev)
+        out["truncated"] = torch.empty((K, N), dtype=torch.bool, device=dev)
+    a = torch.empty((K, N, env.action_dim), dtype=env.act_dtype, device=dev) if actions else None
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    _capi.check(env._lib.invsim_rollout_policy(
+        env._h, int(K), C.byref(spec), p(o), p(out.get("reward")), p(out.get("terminated")),
+        p(out.get("truncated")), p(a), p(metrics), env._stream()), env._h, "rollout_policy")
+    del keep
+    if obs:
+        out["obs"] = o
+    if actions:
+        out["actions"] = a
+    return out
+
+
+def metrics_dim(env):
+    d = C.c_int32()
+    _capi.check(env._lib.invsim_metrics_dim(env._h, C.byref(d)), env._h, "metrics_dim")
+    return d.value
+
+
+def summarize(family, m, main_nodes=None):
+    """Per-episode summary columns from the accumulated sums, with the
+    reference's float expressions."""
+    m = np.asarray(m, np.float64)
+    rows = {"TotalReward": m[:, 0], "Steps": m[:, 1].astype(np.int64)}
+    if family == _capi.INVSIM_INVMGMT:
+        # benchmark_InvManagementBacklogEnv.py:412-415
+        steps, dem, sales, stock, inv = m[:, 1], m[:, 2], m[:, 3], m[:, 4], m[:, 5]
+        rows["AvgServiceLevel"] = np.array([s / max(1e-6, d) if d > 1e-6 else 1.0 for s, d in zip(sales, dem)])
+        rows["TotalStockoutQty"] = stock
+        rows["AvgEndingInv"] = np.array([i / n if n > 0 else 0 for i, n in zip(inv, steps)], np.float64)
+    elif family == _capi.INVSIM_NETINVMGMT:
+        # benchmark_NetInvMgmtLostSalesEnv.py:291-296: DataFrame sums / mean of column means
+        steps, dem, sales, stock = m[:, 1], m[:, 2], m[:, 3], m[:, 4]
+        X = m[:, 5:]
+        rows["AvgServiceLevel"] = np.array([s / max(1e-6, d) if d > 1e-6 else 1.0 for s, d in zip(sales, dem)])
+        rows["TotalStockoutQty"] = stock
+        rows["AvgEndingInv"] = np.array([np.sum(x / n) / x.shape[0] if n > 0 else np.nan
+                                         for x, n in zip(X, steps)])
+    return rows
+
+
+def evaluate_agent(agent, env_cls, env_config=None, n_episodes=100, seed_offset=0, device=None):
+    """Batched evaluate_agent: episode i = env i seeded seed_offset + i, one
+    full episode under ``agent`` in one kernel launch.  Returns a dict of
+    per-episode columns (the reference's summary DataFrame columns)."""
+    env = env_cls(num_envs=n_episodes, device=device, autoreset_mode="disabled", **(env_config or {}))
+    try:
+        env.reset(seed=seed_offset)
+        M = metrics_dim(env)
+        met = torch.zeros((n_episodes, M), dtype=torch.float64, device=env.device)
+        torch.cuda.synchronize(env.device)
+        t0 = time.perf_counter()
+        rollout_policy(env, agent, env._horizon(), obs=False, rewards=False, metrics=met)
+        torch.cuda.synchronize(env.device)
+        dt = time.perf_counter() - t0
+        cols = summarize(env.family, met.cpu().numpy())
+        n = n_episodes
+        out = {"Agent": [agent.name] * n, "Episode": np.arange(1, n + 1), **cols,
+               "Time": np.full(n, dt / max(n, 1)), "Seed": seed_offset + np.arange(n), "Error": [None] * n}
+        return out
+    finally:
+        env.close()

@@ -221,6 +221,12 @@ class InvSimVectorEnv:
                     self._h, "rollout")
         return obs, rew, term, trunc
 
+    def rollout_policy(self, agent, K, obs=False, rewards=True, actions=False, metrics=None):
+        """K steps with the agent's actions computed in the kernel (see
+        invsim.policies); outputs optional, metrics [N, M] accumulated."""
+        from .policies import rollout_policy
+        return rollout_policy(self, agent, K, obs=obs, rewards=rewards, actions=actions, metrics=metrics)
+
     def status(self, clear=True):
         """Sticky device status word (synchronous): bit 0 = an env was stepped past its
         horizon with autoreset disabled after a masked reset (the step was not applied)."""

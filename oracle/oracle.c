@@ -699,7 +699,7 @@ static double py_max0(double x) { return (x > 0) ? x : 0.0; } /* max(0, x) */
 
 /* step :436-635 */
 void orc_net_step(void *p, const float *action, float *obs, double *reward, uint8_t *truncated,
-                  double *Xo, double *Uo, double *Do, double *Ro, double *Yo, double *Po) {
+                  double *Xo, double *Uo, double *Do, double *Ro, double *Yo, double *Po, double *So) {
     net_t *h = (net_t *)p;
     const int J = h->J, EE = h->E, RL = h->RL;
     const int E = EE ? EE : 1, RLs = RL ? RL : 1, SL = h->E + h->RL + 1;
@@ -768,6 +768,7 @@ void orc_net_step(void *p, const float *action, float *obs, double *reward, uint
             double inv = py_max0(xb[node]);
             double sale = (inv < fill) ? inv : fill;       /* min(fill, inv) */
             S[(int64_t)t * SL + EE + r] = sale;
+            if (So) So[i * RLs + r] = sale;
             xb[node] -= sale;
             double unf = fill - sale;
             U[(int64_t)(t + 1) * RLs + r] = h->backlog ? unf : 0.0;

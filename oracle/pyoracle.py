@@ -58,7 +58,7 @@ def _lib():
     lib.orc_nv_step.argtypes = [P] * 6
     lib.orc_nv_get_params.argtypes = [P, P]
     lib.orc_im_step.argtypes = [P] * 10
-    lib.orc_net_step.argtypes = [P] * 11
+    lib.orc_net_step.argtypes = [P] * 12
     lib.orc_net_obs_dim.argtypes = [P]
     lib.orc_net_obs_dim.restype = C.c_int32
     return lib
@@ -395,11 +395,12 @@ class OracleNet(_Base):
         rew = np.zeros(self.n, np.float64)
         tr = np.zeros(self.n, np.uint8)
         if not info:
-            lib().orc_net_step(self.h, _p(action), _p(obs), _p(rew), _p(tr), *([None] * 6))
+            lib().orc_net_step(self.h, _p(action), _p(obs), _p(rew), _p(tr), *([None] * 7))
             return obs, rew, tr.astype(bool)
         J, E, RL = self.topo["J"], self.topo["E"], self.topo["RL"]
         X = np.zeros((self.n, J)); U = np.zeros((self.n, RL)); D = np.zeros((self.n, RL))
         R = np.zeros((self.n, E)); Y = np.zeros((self.n, E)); P = np.zeros((self.n, J))
+        S = np.zeros((self.n, RL))
         lib().orc_net_step(self.h, _p(action), _p(obs), _p(rew), _p(tr), _p(X), _p(U), _p(D), _p(R),
-                           _p(Y), _p(P))
-        return obs, rew, tr.astype(bool), dict(X=X, U=U, D=D, R=R, Y=Y, P=P)
+                           _p(Y), _p(P), _p(S))
+        return obs, rew, tr.astype(bool), dict(X=X, U=U, D=D, R=R, Y=Y, P=P, S=S)
