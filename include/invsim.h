@@ -84,7 +84,8 @@ typedef struct {
     int32_t num_stages;              /* m = len(I0) + 1, 2..9 */
     int32_t periods;
     int32_t backlog;                 /* 1 = InvManagementBacklogEnv, 0 = LostSales */
-    int32_t dist;                    /* 1 = Poisson(mu); 5 = user_D */
+    int32_t dist;                    /* 1 Poisson(mu), 2 binomial(n, p), 3 integers(low, high + 1),
+                                        4 geometric(p), 5 user_D  (inventory_management.py:169-184) */
     double mu;                       /* dist_param['mu'] */
     double alpha;                    /* discount; reward *= alpha**t */
     const int64_t *I0;               /* [m-1] */
@@ -95,6 +96,9 @@ typedef struct {
     const int64_t *supply_capacity;  /* [m-1] = c */
     const int64_t *lead_time;        /* [m-1] = L, each 0..255 */
     const int64_t *user_D;           /* [periods], dist == 5 only (else NULL) */
+    int64_t dist_n;                  /* dist 2: dist_param['n'] */
+    double dist_p;                   /* dist 2, 4: dist_param['p'] */
+    int64_t dist_low, dist_high;     /* dist 3: dist_param['low'], ['high'] (inclusive) */
 } invsim_invmgmt_spec;
 
 /* network_management.py:146-195 classification, compiled to index tables by

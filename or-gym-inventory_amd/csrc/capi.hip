@@ -129,6 +129,7 @@ void bind_common(invsim_handle *h, int64_t o_rng, int64_t o_period, int64_t o_st
     c.period = at<int32_t>(h, o_period);
     c.status = at<uint32_t>(h, o_status);
     c.info_demand = nullptr;
+    c.u32buf = nullptr;
 }
 
 // "done" marker: period = horizon, so NEXT_STEP autoreset resets on first step
@@ -305,8 +306,14 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
         if (!(s->mu >= 0) || s->mu > 1e18) return fail(nullptr, INVSIM_EINVAL, "poisson mu out of range");
     } else if (s->dist == 5) {
         if (!s->user_D) return fail(nullptr, INVSIM_EINVAL, "User specified demand length != num periods");
-    } else if (s->dist >= 2 && s->dist <= 4) {
-        return fail(nullptr, INVSIM_EINVAL, "dist 2/3/4 (binomial/randint/geometric) not implemented on device");
+    } else if (s->dist == 2) {   // numpy Generator.binomial argument checks
+        if (s->dist_n < 0) return fail(nullptr, INVSIM_EINVAL, "n < 0");
+        if (!(s->dist_p >= 0 && s->dist_p <= 1)) return fail(nullptr, INVSIM_EINVAL, "p < 0, p > 1 or p is NaN");
+    } else if (s->dist == 3) {   // Generator.integers(low, high + 1)
+        if (s->dist_high == INT64_MAX) return fail(nullptr, INVSIM_EINVAL, "high is out of bounds for int64");
+        if (s->dist_low > s->dist_high) return fail(nullptr, INVSIM_EINVAL, "low >= high");
+    } else if (s->dist == 4) {   // Generator.geometric
+        if (!(s->dist_p > 0 && s->dist_p <= 1)) return fail(nullptr, INVSIM_EINVAL, "p <= 0, p > 1 or p contains NaNs");
     } else {
         return fail(nullptr, INVSIM_EINVAL, "dist must be one of 1, 2, 3, 4, 5");
     }
@@ -337,6 +344,9 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
     int64_t o_B = lay.add("B", 8, h->im_backlog ? m : 1, h->Npad);
     int64_t o_R = lay.add("Rring", 8, std::max(sumL, 1), h->Npad);
     int64_t o_A = lay.add("alog", 8, std::max(D * m1, 1), h->Npad);
+    // Generator.integers draws 32-bit halves: the bit generator's buffered half is
+    // state (the dist 2-4 kernel variant carries the row; only dist 3 uses it)
+    const int64_t o_U32 = (s->dist >= 2 && s->dist <= 4) ? lay.add("u32buf", 8, 1, h->Npad) : -1;
     // read-only tables: alpha**t (Python float pow == C pow), user_D
     Blob tb;
     std::vector<double> ap((size_t)s->periods);
@@ -353,9 +363,13 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
     if (rc == INVSIM_OK) rc = upload_tables(h, tb.b);
     if (rc == INVSIM_OK) {
         bind_common(h, o_rng, o_per, o_st, ar);
+        if (o_U32 >= 0) h->cm.u32buf = at<uint64_t>(h, o_U32);
         ImParams &p = h->im;
         p.rhs = pc.nk > 0 ? tab<double>(h, o_rhs) : nullptr;
         p.cm = h->cm;
+        if (s->dist == 2) p.nd = np_dist_binomial(s->dist_n, s->dist_p);
+        if (s->dist == 3) p.nd = np_dist_integers(s->dist_low, s->dist_high);
+        if (s->dist == 4) p.nd = np_dist_geometric(s->dist_p);
         p.periods = s->periods;
         p.lt_max = D;
         p.dist = s->dist;

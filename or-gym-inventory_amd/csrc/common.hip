@@ -22,6 +22,7 @@ seed_range_kernel(Common cm, uint64_t base_lo, uint64_t base_hi, int64_t first, 
     Pcg g;
     seed_pcg64(w, nw, g);
     cm.rng.store_all(e, g);
+    if (cm.u32buf) cm.u32buf[e] = 0;   // a new Generator: pcg64 has_uint32 = 0
 }
 
 __global__ void __launch_bounds__(256)
@@ -35,6 +36,7 @@ seed_words_kernel(Common cm, const uint32_t *words, const int32_t *nwords, const
     Pcg g;
     seed_pcg64(w, nw, g);
     cm.rng.store_all(e, g);
+    if (cm.u32buf) cm.u32buf[e] = 0;   // a new Generator: pcg64 has_uint32 = 0
 }
 
 __global__ void __launch_bounds__(256) period_fill_kernel(Common cm, int32_t t) {

@@ -52,6 +52,7 @@ __device__ __forceinline__ int64_t min_via_f64(int64_t a, int64_t sup) {
 template <int M1, bool BACKLOG>
 struct ImState {
     Pcg g;
+    uint64_t u32;        // PCG64 32-bit buffer (dist 3 only)
     int64_t I[M1];
     int64_t B[M1 + 1];
 };
@@ -72,7 +73,7 @@ __device__ __forceinline__ void im_reset_regs(const ImParams &P, ImState<M1, BAC
 }
 
 // One step (:224-352) at period t < periods.  Returns truncated.
-template <int M1, bool BACKLOG>
+template <int M1, bool BACKLOG, bool NPD>
 __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool valid, int j, int t,
                                              ImState<M1, BACKLOG> &s,
                                              const int64_t *__restrict__ arow, int64_t *orow,
@@ -128,7 +129,7 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
 #ifdef INVSIM_ABL_NO_POISSON  // profiling ablation build only (wrong results)
     int64_t d = 20 + (int64_t)(s.g.lo & 3);
 #else
-    int64_t d = (P.dist == 5) ? udem : env_poisson(s.g, P.pc, rhs);
+    int64_t d = NPD ? np_demand(s.g, s.u32, P.nd) : (P.dist == 5) ? udem : env_poisson(s.g, P.pc, rhs);
 #endif
     if (d < 0) d = 0;
     TPROBE(2);
@@ -254,7 +255,7 @@ __device__ __forceinline__ void im_base_stock(const ImParams &P, const PolicyIO 
 
 // Step k of a launch for the wave's envs: step (or NEXT_STEP reset) into the
 // LDS obs tile, SAME_STEP final-obs/reset, then the tile's coalesced store.
-template <int M1, bool BACKLOG, bool STEP_ONLY, bool POL>
+template <int M1, bool BACKLOG, bool STEP_ONLY, bool POL, bool NPD>
 __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<int64_t, int64_t> &io, int k,
                                                int64_t e, int64_t e0, int lane, bool valid, int nvalid,
                                                ImState<M1, BACKLOG> &st, int &t, bool &fault,
@@ -308,7 +309,7 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
             }
             arow = pact;
         }
-        tr = im_step_regs<M1, BACKLOG>(P, e, valid, j, t, st, arow, trow, rhs, ts, apow, udem, r, d,
+        tr = im_step_regs<M1, BACKLOG, NPD>(P, e, valid, j, t, st, arow, trow, rhs, ts, apow, udem, r, d,
                                        POL ? met : nullptr);
         if (POL) {
             met[0] += r;                                            // episode_reward += reward
@@ -343,7 +344,7 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
     wave_lds_sync();
 }
 
-template <int M1, bool BACKLOG, bool TU, bool ONE, bool POL>
+template <int M1, bool BACKLOG, bool TU, bool ONE, bool POL, bool NPD>
 __global__ void __launch_bounds__(WAVE)
 im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
@@ -405,6 +406,7 @@ im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     // env's PCG64 stream (an all-zero stream would never leave the PTRS loop)
     ImState<M1, BACKLOG> st;
     st.g = P.cm.rng.load(valid ? e : N - 1);
+    st.u32 = NPD ? P.cm.u32buf[valid ? e : N - 1] : 0;
 #pragma unroll
     for (int i = 0; i < M1; i++) st.I[i] = P.I[i * S + e];
 #pragma unroll
@@ -416,16 +418,17 @@ im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io, PolicyIO pol) {
 #pragma unroll
     for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[(valid ? e : N - 1) * MD + q] : 0.0;
     if (ONE) {
-        im_launch_step<M1, BACKLOG, TU, false>(P, io, 0, e, e0, lane, valid, nvalid, st, t, fault, im_tile, trow,
+        im_launch_step<M1, BACKLOG, TU, false, NPD>(P, io, 0, e, e0, lane, valid, nvalid, st, t, fault, im_tile, trow,
                                                rhs_l, &ts, &apow0, &udem0, pol, met);
     } else {
         ts.flush(lane);
         for (int k = 0; k < io.K; k++)
-            im_launch_step<M1, BACKLOG, false, POL>(P, io, k, e, e0, lane, valid, nvalid, st, t, fault, im_tile,
+            im_launch_step<M1, BACKLOG, false, POL, NPD>(P, io, k, e, e0, lane, valid, nvalid, st, t, fault, im_tile,
                                                     trow, rhs_l, nullptr, nullptr, nullptr, pol, met);
     }
     if (valid && leader) {
         P.cm.rng.store_state(e, st.g);
+        if (NPD) P.cm.u32buf[e] = st.u32;
 #pragma unroll
         for (int i = 0; i < M1; i++) st_store(P.I + i * S + e, st.I[i]);
         if (BACKLOG) {
@@ -488,8 +491,14 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
-#define K_(M, B, TU, ONE, POL) \
-    hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
+    const bool npd = p.dist >= 2 && p.dist <= 4;
+#define K_(M, B, TU, ONE, POL)                                                                          \
+    do {                                                                                                \
+        if (npd)                                                                                        \
+            hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL, true>), grid, block, lds, s, p, t_u, io, pv);  \
+        else                                                                                            \
+            hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL, false>), grid, block, lds, s, p, t_u, io, pv); \
+    } while (0)
 #define L_(M, B)                                             \
     do {                                                     \
         if (pol) {                                           \

@@ -9,6 +9,7 @@
 
 #include "device_common.hpp"
 #include "group_rng.hpp"
+#include "numpy_dists.hpp"
 
 namespace invsim {
 
@@ -46,6 +47,7 @@ struct Common {
     int32_t *period; // [N] step counter within the episode
     int64_t *info_demand;  // optional [N][demand_dim]
     uint32_t *status;      // sticky error word (DISABLED-mode overrun)
+    uint64_t *u32buf;      // [Npad] PCG64 32-bit output buffer (has << 32 | value), or null
 };
 
 // ---------------------------------------------------------------- Newsvendor
@@ -66,7 +68,8 @@ struct ImParams {
     Common cm;
     int32_t periods;
     int32_t lt_max;              // D = max lead time (obs window rows)
-    int32_t dist;                // 1 poisson, 5 user_D
+    int32_t dist;                // 1 poisson, 2 binomial, 3 integers, 4 geometric, 5 user_D
+    NpDist nd;                   // dist 2-4 constants (numpy_dists.hpp)
     int32_t L[IM_MAX_M1];
     int32_t ring_off[IM_MAX_M1]; // first R-ring row of stage i (depth L[i])
     int64_t c[IM_MAX_M1];

@@ -41,7 +41,8 @@ class InvMgmtSpec(C.Structure):
                 ("dist", C.c_int32), ("mu", C.c_double), ("alpha", C.c_double),
                 ("I0", C.c_void_p), ("unit_price", C.c_void_p), ("unit_cost", C.c_void_p),
                 ("demand_cost", C.c_void_p), ("holding_cost", C.c_void_p),
-                ("supply_capacity", C.c_void_p), ("lead_time", C.c_void_p), ("user_D", C.c_void_p)]
+                ("supply_capacity", C.c_void_p), ("lead_time", C.c_void_p), ("user_D", C.c_void_p),
+                ("dist_n", C.c_int64), ("dist_p", C.c_double), ("dist_low", C.c_int64), ("dist_high", C.c_int64)]
 
 
 NET_TABLE_FIELDS = ("I0", "h", "C", "o", "v", "is_factory", "is_retail", "sup", "pur",

@@ -98,12 +98,18 @@ class InvManagementMasterEnv(InvSimVectorEnv):
             c=np.ascontiguousarray(self.supply_capacity), L=np.ascontiguousarray(self.lead_time),
             uD=np.ascontiguousarray(self.user_D if self.dist == 5 else np.zeros(1, np.int64)))
         k = self._keep
-        mu = float(self.dist_param["mu"]) if self.dist == 1 else 0.0
+        dp = self.dist_param
+        mu = float(dp["mu"]) if self.dist == 1 else 0.0
+        # dist_param keys the reference's samplers read (:173-182); a missing key
+        # raises KeyError here rather than at the first step
+        dn = int(dp["n"]) if self.dist == 2 else 0
+        dpp = float(dp["p"]) if self.dist in (2, 4) else 0.0
+        lo, hi = (int(dp["low"]), int(dp["high"])) if self.dist == 3 else (0, 0)
         self._spec = _capi.InvMgmtSpec(
             m, self.num_periods, int(self.backlog), int(self.dist), mu, float(self.alpha),
             k["I0"].ctypes.data, k["up"].ctypes.data, k["uc"].ctypes.data, k["kc"].ctypes.data,
             k["hc"].ctypes.data, k["c"].ctypes.data, k["L"].ctypes.data,
-            k["uD"].ctypes.data if self.dist == 5 else None)
+            k["uD"].ctypes.data if self.dist == 5 else None, dn, dpp, lo, hi)
         self._create_handle(self._lib.invsim_create_invmgmt, self._spec)
 
     def _horizon(self):

@@ -172,6 +172,228 @@ void orc_poisson_fill(uint64_t rng[4], double lam, int64_t *out, int64_t n) {
     for (int64_t i = 0; i < n; i++) out[i] = orc_poisson(rng, lam);
 }
 
+/* ---- numpy Generator.integers / binomial / geometric (numpy 2.2.6,
+ * random/src/distributions/distributions.c + pcg64.h), the demand samplers of
+ * inventory_management.py:173-182 (dist 2, 3, 4). */
+
+/* pcg64_next32: the low half of a 64-bit output first, the high half buffered
+ * in the bit generator (has_uint32 / uinteger) for the next 32-bit draw */
+uint32_t orc_next32(uint64_t rng[4], uint32_t *buf /* [2]: has, value */) {
+    if (buf[0]) {
+        buf[0] = 0;
+        return buf[1];
+    }
+    uint64_t x = orc_next64(rng);
+    buf[0] = 1;
+    buf[1] = (uint32_t)(x >> 32);
+    return (uint32_t)x;
+}
+
+/* random_bounded_uint64_fill(cnt = 1, use_masked = false): off + [0, rng] via
+ * Lemire's method (32-bit buffered draws when rng fits in 32 bits) */
+uint64_t orc_bounded_uint64(uint64_t rng[4], uint32_t *buf, uint64_t off, uint64_t r) {
+    if (r == 0) return off;
+    if (r <= 0xFFFFFFFFULL) {
+        if (r == 0xFFFFFFFFULL) return off + orc_next32(rng, buf);
+        const uint32_t rng_excl = (uint32_t)r + 1;
+        uint64_t m = (uint64_t)orc_next32(rng, buf) * rng_excl;
+        uint32_t leftover = (uint32_t)m;
+        if (leftover < rng_excl) {
+            const uint32_t threshold = (uint32_t)((UINT32_MAX - (uint32_t)r) % rng_excl);
+            while (leftover < threshold) {
+                m = (uint64_t)orc_next32(rng, buf) * rng_excl;
+                leftover = (uint32_t)m;
+            }
+        }
+        return off + (m >> 32);
+    }
+    if (r == 0xFFFFFFFFFFFFFFFFULL) return off + orc_next64(rng);
+    const uint64_t rng_excl = r + 1;
+    u128 m = (u128)orc_next64(rng) * rng_excl;
+    uint64_t leftover = (uint64_t)m;
+    if (leftover < rng_excl) {
+        const uint64_t threshold = (UINT64_MAX - r) % rng_excl;
+        while (leftover < threshold) {
+            m = (u128)orc_next64(rng) * rng_excl;
+            leftover = (uint64_t)m;
+        }
+    }
+    return off + (uint64_t)(m >> 64);
+}
+
+/* Generator.integers(low, high) (high exclusive, int64) */
+int64_t orc_integers(uint64_t rng[4], uint32_t *buf, int64_t low, int64_t high) {
+    const uint64_t r = (uint64_t)high - (uint64_t)low - 1;
+    return (int64_t)orc_bounded_uint64(rng, buf, (uint64_t)low, r);
+}
+
+/* random_binomial_inversion (n * p <= 30) */
+static int64_t binomial_inversion(uint64_t rng[4], int64_t n, double p) {
+    const double q = 1.0 - p;
+    const double qn = exp(n * log(q));
+    const double np = n * p;
+    const int64_t bound = (int64_t)fmin((double)n, np + 10.0 * sqrt(np * q + 1));
+    int64_t X = 0;
+    double px = qn;
+    double U = orc_next_double(rng);
+    while (U > px) {
+        X++;
+        if (X > bound) {
+            X = 0;
+            px = qn;
+            U = orc_next_double(rng);
+        } else {
+            U -= px;
+            px = ((n - X + 1) * p * px) / (X * q);
+        }
+    }
+    return X;
+}
+
+/* random_binomial_btpe (n * p > 30, p <= 0.5) */
+static int64_t binomial_btpe(uint64_t rng[4], int64_t n, double p) {
+    const double r = fmin(p, 1.0 - p);
+    const double q = 1.0 - r;
+    const double fm = n * r + r;
+    const int64_t m = (int64_t)floor(fm);
+    const double p1 = floor(2.195 * sqrt(n * r * q) - 4.6 * q) + 0.5;
+    const double xm = m + 0.5;
+    const double xl = xm - p1;
+    const double xr = xm + p1;
+    const double c = 0.134 + 20.5 / (15.3 + m);
+    double a = (fm - xl) / (fm - xl * r);
+    const double laml = a * (1.0 + a / 2.0);
+    a = (xr - fm) / (xr * q);
+    const double lamr = a * (1.0 + a / 2.0);
+    const double p2 = p1 * (1.0 + 2.0 * c);
+    const double p3 = p2 + c / laml;
+    const double p4 = p3 + c / lamr;
+    double u, v, x, s, F, rho, t, A, x1, x2, f1, f2, z, z2, w, w2, nrq;
+    int64_t y, k, i;
+step10:
+    nrq = n * r * q;
+    u = orc_next_double(rng) * p4;
+    v = orc_next_double(rng);
+    if (u > p1) goto step20;
+    y = (int64_t)floor(xm - p1 * v + u);
+    goto step60;
+step20:
+    if (u > p2) goto step30;
+    x = xl + (u - p1) / c;
+    v = v * c + 1.0 - fabs(m - x + 0.5) / p1;
+    if (v > 1.0) goto step10;
+    y = (int64_t)floor(x);
+    goto step50;
+step30:
+    if (u > p3) goto step40;
+    y = (int64_t)floor(xl + log(v) / laml);
+    if ((y < 0) || (v == 0.0)) goto step10;
+    v = v * (u - p2) * laml;
+    goto step50;
+step40:
+    y = (int64_t)floor(xr - log(v) / lamr);
+    if ((y > n) || (v == 0.0)) goto step10;
+    v = v * (u - p3) * lamr;
+step50:
+    k = llabs(y - m);
+    if ((k > 20) && (k < ((nrq) / 2.0 - 1))) goto step52;
+    s = r / q;
+    a = s * (n + 1);
+    F = 1.0;
+    if (m < y) {
+        for (i = m + 1; i <= y; i++) F *= (a / i - s);
+    } else if (m > y) {
+        for (i = y + 1; i <= m; i++) F /= (a / i - s);
+    }
+    if (v > F) goto step10;
+    goto step60;
+step52:
+    rho = (k / (nrq)) * ((k * (k / 3.0 + 0.625) + 0.16666666666666666) / nrq + 0.5);
+    t = -k * k / (2 * nrq);
+    A = log(v);
+    if (A < (t - rho)) goto step60;
+    if (A > (t + rho)) goto step10;
+    x1 = y + 1;
+    f1 = m + 1;
+    z = n + 1 - m;
+    w = n - y + 1;
+    x2 = x1 * x1;
+    f2 = f1 * f1;
+    z2 = z * z;
+    w2 = w * w;
+    if (A > (xm * log(f1 / x1) + (n - m + 0.5) * log(z / w) + (y - m) * log(w * r / (x1 * q)) +
+             (13680. - (462. - (132. - (99. - 140. / f2) / f2) / f2) / f2) / f1 / 166320. +
+             (13680. - (462. - (132. - (99. - 140. / z2) / z2) / z2) / z2) / z / 166320. +
+             (13680. - (462. - (132. - (99. - 140. / x2) / x2) / x2) / x2) / x1 / 166320. +
+             (13680. - (462. - (132. - (99. - 140. / w2) / w2) / w2) / w2) / w / 166320.))
+        goto step10;
+step60:
+    if (p > 0.5) y = n - y;
+    return y;
+}
+
+/* random_binomial */
+int64_t orc_binomial(uint64_t rng[4], int64_t n, double p) {
+    if ((n == 0) || (p == 0.0f)) return 0;
+    if (p <= 0.5) {
+        if (p * n <= 30.0) return binomial_inversion(rng, n, p);
+        return binomial_btpe(rng, n, p);
+    }
+    const double q = 1.0 - p;
+    if (q * n <= 30.0) return n - binomial_inversion(rng, n, q);
+    return n - binomial_btpe(rng, n, q);
+}
+
+#include "numpy_ziggurat.h"
+
+/* random_standard_exponential (256-level ziggurat, tables from numpy) */
+double orc_standard_exponential(uint64_t rng[4]) {
+    for (;;) {
+        uint64_t ri = orc_next64(rng);
+        ri >>= 3;
+        const uint8_t idx = (uint8_t)(ri & 0xFF);
+        ri >>= 8;
+        const double x = ri * npz_we[idx];
+        if (ri < npz_ke[idx]) return x;
+        if (idx == 0) return NPZ_EXP_R - log1p(-orc_next_double(rng));
+        if ((npz_fe[idx - 1] - npz_fe[idx]) * orc_next_double(rng) + npz_fe[idx] < exp(-x)) return x;
+    }
+}
+
+/* random_geometric: search for p >= 1/3, else inversion of the exponential */
+int64_t orc_geometric(uint64_t rng[4], double p) {
+    if (p >= 0.333333333333333333333333) {
+        int64_t X = 1;
+        double sum = p, prod = p;
+        const double q = 1.0 - p;
+        const double U = orc_next_double(rng);
+        while (U > sum) {
+            prod *= q;
+            sum += prod;
+            X++;
+        }
+        return X;
+    }
+    const double z = ceil(-orc_standard_exponential(rng) / log1p(-p));
+    if (z >= 9.223372036854776e+18) return INT64_MAX;
+    return (int64_t)z;
+}
+
+void orc_dist_fill(uint64_t rng[4], uint32_t *buf, int dist, int64_t n_or_low, int64_t high, double p,
+                   int64_t *out, int64_t count) {
+    for (int64_t i = 0; i < count; i++) {
+        if (dist == 2) out[i] = orc_binomial(rng, n_or_low, p);
+        else if (dist == 3) out[i] = orc_integers(rng, buf, n_or_low, high);
+        else if (dist == 4) out[i] = orc_geometric(rng, p);
+        else out[i] = 0;
+    }
+}
+
+double orc_exponential_fill(uint64_t rng[4], double *out, int64_t count) {
+    for (int64_t i = 0; i < count; i++) out[i] = orc_standard_exponential(rng);
+    return 0.0;
+}
+
 /* numpy add.reduce for float32/float64 1-D contiguous input: identity 0 then
  * pairwise_sum (loops_utils.h.src): n<8 sequential; n<=128 eight accumulators;
  * else split at n/2 rounded down to a multiple of 8. */
@@ -388,6 +610,9 @@ void orc_nv_step(void *p, const float *action, float *obs, double *reward, uint8
 typedef struct {
     int32_t m, m1, T, lt_max, O, backlog, dist;
     double mu, alpha;
+    int64_t dn, dlow, dhigh;
+    double dp;
+    uint32_t *u32; /* per env [2]: the bit generator's buffered 32-bit half */
     int64_t *I0, *c, *L, *user_D;
     double up[64], uc[64], kc[64], hc[64]; /* f32 coefficients widened exactly */
     int64_t n;
@@ -405,6 +630,10 @@ void *orc_im_create(const orc_im_cfg *cfg, int64_t n) {
     h->dist = cfg->dist;
     h->mu = cfg->mu;
     h->alpha = cfg->alpha;
+    h->dn = cfg->dist_n;
+    h->dp = cfg->dist_p;
+    h->dlow = cfg->dist_low;
+    h->dhigh = cfg->dist_high;
     h->I0 = (int64_t *)malloc(sizeof(int64_t) * h->m1);
     h->c = (int64_t *)malloc(sizeof(int64_t) * h->m1);
     h->L = (int64_t *)malloc(sizeof(int64_t) * h->m1);
@@ -432,11 +661,13 @@ void *orc_im_create(const orc_im_cfg *cfg, int64_t n) {
     h->B = (int64_t *)calloc((size_t)n * (h->T + 1) * h->m, sizeof(int64_t));
     h->alog = (int64_t *)calloc((size_t)n * (h->T + 1) * h->m1, sizeof(int64_t));
     h->period = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+    h->u32 = (uint32_t *)calloc((size_t)n * 2, sizeof(uint32_t));
     return h;
 }
 
 void orc_im_destroy(void *p) {
     im_t *h = (im_t *)p;
+    free(h->u32);
     free(h->I0); free(h->c); free(h->L); free(h->user_D);
     free(h->rng); free(h->I); free(h->R); free(h->B); free(h->alog); free(h->period);
     free(h);
@@ -444,7 +675,10 @@ void orc_im_destroy(void *p) {
 
 void orc_im_seed(void *p, const uint32_t *words, const int32_t *nwords) {
     im_t *h = (im_t *)p;
-    for (int64_t i = 0; i < h->n; i++) orc_seed_pcg64(words + 4 * i, nwords[i], h->rng + 4 * i);
+    for (int64_t i = 0; i < h->n; i++) {
+        orc_seed_pcg64(words + 4 * i, nwords[i], h->rng + 4 * i);
+        h->u32[2 * i] = 0;   /* a new Generator: has_uint32 = 0 */
+    }
 }
 
 /* _get_obs :354-391 */
@@ -524,6 +758,12 @@ void orc_im_step(void *p, const int64_t *action, int64_t *obs, double *reward, u
         int64_t d;
         if (h->dist == 5)
             d = t < h->T ? h->user_D[t] : 0;                          /* :182 */
+        else if (h->dist == 2)
+            d = orc_binomial(rng, h->dn, h->dp);                      /* :175 */
+        else if (h->dist == 3)
+            d = orc_integers(rng, h->u32 + 2 * i, h->dlow, h->dhigh + 1); /* :178 */
+        else if (h->dist == 4)
+            d = orc_geometric(rng, h->dp);                            /* :181 */
         else
             d = orc_poisson(rng, h->mu);                              /* :172 */
         if (d < 0) d = 0;                                             /* :280 */

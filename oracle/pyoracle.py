@@ -43,6 +43,9 @@ def _lib():
     lib.orc_poisson.argtypes = [P, C.c_double]
     lib.orc_poisson.restype = C.c_int64
     lib.orc_poisson_fill.argtypes = [P, C.c_double, P, C.c_int64]
+    lib.orc_dist_fill.argtypes = [P, P, C.c_int, C.c_int64, C.c_int64, C.c_double, P, C.c_int64]
+    lib.orc_exponential_fill.argtypes = [P, P, C.c_int64]
+    lib.orc_exponential_fill.restype = C.c_double
     lib.orc_loggam.argtypes = [C.c_double]
     lib.orc_loggam.restype = C.c_double
     lib.orc_sum_f32.argtypes = [P, C.c_int64]
@@ -113,6 +116,23 @@ def poisson_stream(seed, lam, n):
     return out, st
 
 
+def dist_stream(seed, dist, n, n_or_low=0, high=0, p=0.0):
+    """numpy Generator(PCG64(seed)) draws: dist 2 binomial(n_or_low, p),
+    3 integers(n_or_low, high), 4 geometric(p).  Returns (draws, state, buf)."""
+    st = pcg64_init(seed)
+    buf = np.zeros(2, np.uint32)
+    out = np.zeros(n, np.int64)
+    lib().orc_dist_fill(_p(st), _p(buf), int(dist), int(n_or_low), int(high), float(p), _p(out), n)
+    return out, st, buf
+
+
+def exponential_stream(seed, n):
+    st = pcg64_init(seed)
+    out = np.zeros(n, np.float64)
+    lib().orc_exponential_fill(_p(st), _p(out), n)
+    return out, st
+
+
 # ---------------------------------------------------------------- structs
 class NVCfg(C.Structure):
     _fields_ = [("lead_time", C.c_int32), ("step_limit", C.c_int32),
@@ -126,7 +146,8 @@ class IMCfg(C.Structure):
                 ("dist", C.c_int32), ("mu", C.c_double), ("alpha", C.c_double),
                 ("I0", C.c_void_p), ("unit_price", C.c_void_p), ("unit_cost", C.c_void_p),
                 ("demand_cost", C.c_void_p), ("holding_cost", C.c_void_p),
-                ("supply_capacity", C.c_void_p), ("lead_time", C.c_void_p), ("user_D", C.c_void_p)]
+                ("supply_capacity", C.c_void_p), ("lead_time", C.c_void_p), ("user_D", C.c_void_p),
+                ("dist_n", C.c_int64), ("dist_p", C.c_double), ("dist_low", C.c_int64), ("dist_high", C.c_int64)]
 
 
 class NetCfg(C.Structure):
@@ -216,12 +237,15 @@ class OracleInvMgmt(_Base):
         self.lt_max = int(self._keep["L"].max()) if self.m > 1 else 0
         self.obs_dim = (self.m - 1) * (self.lt_max + 1)
         self.periods = int(kw["periods"])
-        mu = float(kw["dist_param"].get("mu", 0)) if kw["dist"] == 1 else 0.0
+        dp, dist = kw["dist_param"], kw["dist"]
+        mu = float(dp.get("mu", 0)) if dist == 1 else 0.0
         k = self._keep
-        self.cfg = IMCfg(self.m, int(kw["periods"]), int(bool(kw["backlog"])), int(kw["dist"]), mu,
+        self.cfg = IMCfg(self.m, int(kw["periods"]), int(bool(kw["backlog"])), int(dist), mu,
                          float(kw["alpha"]), _p(k["I0"]).value, _p(k["up"]).value,
                          _p(k["uc"]).value, _p(k["kc"]).value, _p(k["hc"]).value,
-                         _p(k["c"]).value, _p(k["L"]).value, _p(k["uD"]).value)
+                         _p(k["c"]).value, _p(k["L"]).value, _p(k["uD"]).value,
+                         int(dp["n"]) if dist == 2 else 0, float(dp["p"]) if dist in (2, 4) else 0.0,
+                         int(dp["low"]) if dist == 3 else 0, int(dp["high"]) if dist == 3 else 0)
         self.h = lib().orc_im_create(C.byref(self.cfg), n)
 
     def reset(self):

@@ -47,6 +47,7 @@ def test_spec_struct_layout_matches_header(tmp_path):
         "invsim_newsvendor_spec": (_capi.NewsvendorSpec, [f for f, _ in _capi.NewsvendorSpec._fields_]),
         "invsim_invmgmt_spec": (_capi.InvMgmtSpec, [f for f, _ in _capi.InvMgmtSpec._fields_]),
         "invsim_netinvmgmt_spec": (_capi.NetInvMgmtSpec, [f for f, _ in _capi.NetInvMgmtSpec._fields_]),
+        "invsim_policy": (_capi.PolicySpec, [f for f, _ in _capi.PolicySpec._fields_]),
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for cname, (_, names) in fields.items():
@@ -102,8 +103,15 @@ def test_validation_errors_mirror_reference_asserts():
     assert lib.invsim_create_invmgmt(C.byref(spec), 8, 0, 0, C.byref(h)) == -22
     assert b"alpha" in lib.invsim_last_error(None)
     spec.alpha = 0.97
-    spec.dist = 2
-    assert lib.invsim_create_invmgmt(C.byref(spec), 8, 0, 0, C.byref(h)) == -22
+    # numpy's own argument checks for the demand samplers (inventory_management.py:173-182)
+    for dist, kw, msg in [(2, dict(dist_n=10, dist_p=1.5), b"p > 1"), (2, dict(dist_n=-1, dist_p=0.5), b"n < 0"),
+                          (3, dict(dist_low=5, dist_high=4), b"low >= high"), (4, dict(dist_p=0.0), b"p <= 0"),
+                          (7, {}, b"dist must be one of")]:
+        spec.dist = dist
+        for k, v in kw.items():
+            setattr(spec, k, v)
+        assert lib.invsim_create_invmgmt(C.byref(spec), 8, 0, 0, C.byref(h)) == -22
+        assert msg in lib.invsim_last_error(None)
 
 
 def test_python_env_fails_loudly_without_gpu():

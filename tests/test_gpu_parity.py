@@ -400,3 +400,51 @@ def test_poisson_many_draws_vs_oracle(gpu, oracle):
             g.poisson(20)
         s = g.bit_generator.state["state"]["state"]
         assert int(st[0, i]) == s >> 64 and int(st[1, i]) == s & (2**64 - 1)
+
+
+# ---------------------------------------------------------------- numpy demand samplers (dist 2-4)
+@pytest.mark.parametrize("dist,dp", [(2, {"n": 40, "p": 0.5}), (2, {"n": 400, "p": 0.05}), (2, {"n": 300, "p": 0.8}),
+                                     (2, {"n": 1000, "p": 0.3}), (3, {"low": 0, "high": 40}),
+                                     (3, {"low": -5, "high": 2**40}), (4, {"p": 0.05}), (4, {"p": 0.5}),
+                                     (4, {"p": 1e-4})])
+def test_invmgmt_numpy_dists_vs_oracle(gpu, oracle, dist, dp):
+    from invsim import InvManagementBacklogEnv
+    n = 1000
+    env = InvManagementBacklogEnv(n, device=gpu, dist=dist, dist_param=dp, record_demand=True)
+    orc = oracle.OracleInvMgmt(n, dist=dist, dist_param=dp)
+    orc.seed(range(40, 40 + n))
+    e_obs = orc.reset()
+    obs, _ = env.reset(seed=40)
+    rng = np.random.default_rng(2)
+    for s in range(61):   # two episodes and the NEXT_STEP reset between them
+        a = rng.integers(0, 120, size=(n, 3))
+        o, r, te, tr, info = env.step(torch.from_numpy(a).to(gpu))
+        if s == 30:
+            e_obs = orc.reset()
+            assert np.array_equal(o.cpu().numpy(), e_obs), "autoreset obs"
+            continue
+        e_obs, e_rew, e_tr, e_info = orc.step(a, info=True)
+        assert np.array_equal(info["demand"].cpu().numpy(), e_info["demand"]), f"demand step {s}"
+        assert np.array_equal(o.cpu().numpy(), e_obs), f"obs step {s}"
+        _assert_reward(r.cpu().numpy(), e_rew, f"step {s}")
+
+
+def test_invmgmt_integers_buffer_is_state(gpu):
+    """The PCG64 32-bit half buffered by integers() is env state: it survives a
+    checkpoint round trip and a reset without seed, and re-seeding clears it."""
+    from invsim import InvManagementBacklogEnv
+    n = 300
+    mk = lambda: InvManagementBacklogEnv(n, device=gpu, dist=3, dist_param={"low": 0, "high": 30},  # noqa: E731
+                                         record_demand=True)
+    e1, e2 = mk(), mk()
+    e1.reset(seed=5)
+    a = torch.full((n, 3), 20, dtype=torch.int64, device=gpu)
+    e1.step(a)                                     # one draw: the high half is now buffered
+    e2.set_state(e1.get_state())
+    d1 = [e1.step(a)[4]["demand"].clone() for _ in range(5)]
+    d2 = [e2.step(a)[4]["demand"].clone() for _ in range(5)]
+    assert all(torch.equal(x, y) for x, y in zip(d1, d2))
+    e1.reset(seed=5)
+    e3 = mk()
+    e3.reset(seed=5)
+    assert torch.equal(e1.step(a)[4]["demand"], e3.step(a)[4]["demand"])

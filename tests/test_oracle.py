@@ -157,3 +157,66 @@ def test_golden_coverage_of_quirk_branches():
     assert (fx["U"] == 0).all(), "true lost sales keeps U at 0"
     fx, _ = load_golden("net_lostsales_default")
     assert (fx["U"] > 0).any(), "reference LostSales class runs backlog=True"
+
+
+# ---------------------------------------------------------------- numpy demand samplers (dist 2-4)
+def _npg(seed):
+    return np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+
+
+@pytest.mark.parametrize("seed", [0, 7, 123456])
+def test_standard_exponential_vs_numpy(oracle, seed):
+    a, _ = oracle.exponential_stream(seed, 100000)
+    assert np.array_equal(a.view(np.uint64), _npg(seed).standard_exponential(100000).view(np.uint64))
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 11), (5, 300), (-50, 50), (0, 2**32), (0, 2**32 + 1), (0, 2**40),
+                                   (-2**62, 2**62), (3, 4)])
+def test_integers_vs_numpy(oracle, lo, hi):
+    a, _, _ = oracle.dist_stream(3, 3, 20001, lo, hi)
+    g = _npg(3)
+    assert np.array_equal(a, np.array([g.integers(lo, hi) for _ in range(20001)]))
+
+
+@pytest.mark.parametrize("n,p", [(10, 0.5), (100, 0.2), (100, 0.35), (1000, 0.5), (20, 0.9), (1000, 0.97),
+                                 (50, 0.01), (5000, 0.3), (7, 1.0), (0, 0.3), (40, 0.0)])
+def test_binomial_vs_numpy(oracle, n, p):
+    a, _, _ = oracle.dist_stream(11, 2, 20000, n, 0, p)
+    g = _npg(11)
+    assert np.array_equal(a, np.array([g.binomial(n, p) for _ in range(20000)]))
+
+
+@pytest.mark.parametrize("p", [1.0, 0.5, 0.34, 1 / 3, 0.3333333333333333, 0.2, 0.05, 0.001, 1e-9])
+def test_geometric_vs_numpy(oracle, p):
+    a, _, _ = oracle.dist_stream(5, 4, 20000, 0, 0, p)
+    g = _npg(5)
+    assert np.array_equal(a, np.array([g.geometric(p) for _ in range(20000)]))
+
+
+@pytest.mark.parametrize("dist,dp", [(2, {"n": 40, "p": 0.5}), (2, {"n": 400, "p": 0.05}),
+                                     (3, {"low": 0, "high": 40}), (4, {"p": 0.05}), (4, {"p": 0.5})])
+def test_oracle_invmgmt_demand_stream_is_numpys(oracle, dist, dp):
+    """The env draws np_random.<sampler>(...) once per step (inventory_management.py:173-182,
+    :280): env i's demand sequence is numpy's sequence for seed base + i (the
+    32-bit buffer of integers() carried across steps; reset without seed keeps it)."""
+    n, base = 6, 321
+    orc = oracle.OracleInvMgmt(n, dist=dist, dist_param=dp)
+    orc.seed(range(base, base + n))
+    orc.reset()
+    a = np.full((n, 3), 60, np.int64)
+    dem = []
+    for ep in range(2):
+        if ep:
+            orc.reset()
+        for _ in range(30):
+            dem.append(orc.step(a, info=True)[3]["demand"])
+    dem = np.stack(dem, 1)
+    for i in range(n):
+        g = _npg(base + i)
+        if dist == 2:
+            e = [g.binomial(dp["n"], dp["p"]) for _ in range(60)]
+        elif dist == 3:
+            e = [g.integers(dp["low"], dp["high"] + 1) for _ in range(60)]
+        else:
+            e = [g.geometric(dp["p"]) for _ in range(60)]
+        assert np.array_equal(dem[i], np.maximum(np.array(e), 0)), i
