@@ -227,6 +227,20 @@ int invsim_kernel_variant(const invsim_handle *h, int32_t *variant);
  * written by every subsequent step/rollout(last step) when non-NULL. */
 int invsim_set_info_demand(invsim_handle *h, int64_t *demand);
 
+/* Optional per-step record of the reference's step info (for a single-env
+ * view that keeps the reference's history arrays), written by every
+ * subsequent step/rollout (last step) when non-NULL:
+ *   InvMgmt    int64 [N][2m + 5]:    sales S[t] (m), unfulfilled U[t] (m), then the
+ *                                    float64 bit patterns of period_profit, revenue,
+ *                                    procurement, holding and penalty cost sums
+ *                                    (inventory_management.py:314-345)
+ *   NetInvMgmt f64 [N][2 RL + 2 J + 2 E]: S[t, retail links], U[t+1, retail links],
+ *                                    X[t+1, main nodes], R[t, reorder links], Y[t+1, reorder
+ *                                    links], P[t, main nodes]  (network_management.py:436-619)
+ *   Newsvendor: none (dim 0). */
+int invsim_info_record_dim(const invsim_handle *h, int32_t *dim);
+int invsim_set_info_record(invsim_handle *h, void *record);
+
 /* Checkpoint / debug: the full device state as one opaque blob of state_bytes,
  * plus a field directory (name, byte offset, element size, rows) for tests. */
 int invsim_state_bytes(const invsim_handle *h, int64_t *bytes);

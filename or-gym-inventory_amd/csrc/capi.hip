@@ -130,6 +130,7 @@ void bind_common(invsim_handle *h, int64_t o_rng, int64_t o_period, int64_t o_st
     c.status = at<uint32_t>(h, o_status);
     c.info_demand = nullptr;
     c.u32buf = nullptr;
+    c.info_rec = nullptr;
 }
 
 // "done" marker: period = horizon, so NEXT_STEP autoreset resets on first step
@@ -587,6 +588,26 @@ int invsim_set_autoreset(invsim_handle *h, int32_t mode) {
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (!valid_autoreset(mode)) return fail(h, INVSIM_EINVAL, "bad autoreset mode");
     h->cm.autoreset = mode;
+    sync_common(h);
+    return INVSIM_OK;
+}
+
+static int info_record_dim(const invsim_handle *h) {
+    if (h->family == INVSIM_INVMGMT) return 2 * (h->im_m1 + 1) + 5;
+    if (h->family == INVSIM_NETINVMGMT) return 2 * h->net.RL + 2 * h->net.J + 2 * h->net.E;
+    return 0;
+}
+
+int invsim_info_record_dim(const invsim_handle *h, int32_t *dim) {
+    if (!h || !dim) return fail(nullptr, INVSIM_EINVAL, "null argument");
+    *dim = info_record_dim(h);
+    return INVSIM_OK;
+}
+
+int invsim_set_info_record(invsim_handle *h, void *record) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (record && info_record_dim(h) == 0) return fail(h, INVSIM_EINVAL, "this env family has no step record");
+    h->cm.info_rec = record;
     sync_common(h);
     return INVSIM_OK;
 }

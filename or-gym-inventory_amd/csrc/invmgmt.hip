@@ -78,7 +78,7 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
                                              ImState<M1, BACKLOG> &s,
                                              const int64_t *__restrict__ arow, int64_t *orow,
                                              const double *rhs, TableStage *ts, double apow, int64_t udem,
-                                             double &reward, int64_t &dem_out, double *met) {
+                                             double &reward, int64_t &dem_out, double *met, int64_t *irec) {
     const int64_t S = P.cm.Npad;
     const int D = P.lt_max;
     const bool leader = valid && j == 0;   // state writes
@@ -179,6 +179,28 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
 #pragma unroll
     for (int q = 0; q <= M1; q++) s.B[q] = BACKLOG ? U[q] : 0;      // :307-312
     dem_out = d;
+    if (irec) {  // step info (inventory_management.py:334-345): S[t], U[t], then the
+                 // f64 bits of period_profit, revenue, procurement, holding, penalty sums
+        constexpr int W = 2 * (M1 + 1) + 5;
+        int64_t *rr = irec + e * W;
+#pragma unroll
+        for (int q = 0; q <= M1; q++) {
+            rr[q] = Sv[q];
+            rr[M1 + 1 + q] = U[q];
+        }
+        const double rev = np_sum<double>(M1 + 1, [&](int q) { return P.up[q] * (double)Sv[q]; });
+        const double pro = np_sum<double>(M1 + 1, [&](int q) { return P.uc[q] * (double)Sv[q]; });
+        const double hol = np_sum<double>(M1 + 1, [&](int q) {
+            const int64_t inv = (q < M1) ? Icur[q] : 0;
+            return P.hc[q] * (double)(inv > 0 ? inv : 0);
+        });
+        const double pen = np_sum<double>(M1 + 1, [&](int q) { return P.kc[q] * (double)U[q]; });
+        rr[2 * (M1 + 1) + 0] = __double_as_longlong(profit);
+        rr[2 * (M1 + 1) + 1] = __double_as_longlong(rev);
+        rr[2 * (M1 + 1) + 2] = __double_as_longlong(pro);
+        rr[2 * (M1 + 1) + 3] = __double_as_longlong(hol);
+        rr[2 * (M1 + 1) + 4] = __double_as_longlong(pen);
+    }
     if (met) {   // evaluate_agent metrics (benchmark_InvManagementBacklogEnv.py:378-399)
         met[2] += (double)d;                                        // demand_realized
         met[3] += (double)Sv[0];                                    // sales[0]
@@ -310,7 +332,8 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
             arow = pact;
         }
         tr = im_step_regs<M1, BACKLOG, NPD>(P, e, valid, j, t, st, arow, trow, rhs, ts, apow, udem, r, d,
-                                       POL ? met : nullptr);
+                                            POL ? met : nullptr,
+                                            (valid && leader && k == io.K - 1) ? (int64_t *)P.cm.info_rec : nullptr);
         if (POL) {
             met[0] += r;                                            // episode_reward += reward
             met[1] += 1.0;                                          // episode_steps

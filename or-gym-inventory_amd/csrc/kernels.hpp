@@ -48,6 +48,7 @@ struct Common {
     int64_t *info_demand;  // optional [N][demand_dim]
     uint32_t *status;      // sticky error word (DISABLED-mode overrun)
     uint64_t *u32buf;      // [Npad] PCG64 32-bit output buffer (has << 32 | value), or null
+    void *info_rec;        // optional per-step info record (invsim_set_info_record), last step of a launch
 };
 
 // ---------------------------------------------------------------- Newsvendor

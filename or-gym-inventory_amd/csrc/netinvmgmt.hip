@@ -58,7 +58,8 @@ __device__ __forceinline__ void net_reset_lds(const NetParams &P, NetScratch &s,
 // LDS scratch, lane-group Poisson draws); lane j == 0 writes state and the
 // U/X part of the obs row, lane j writes the order windows of links k = j mod LPE.
 __device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, Pcg &g, NetScratch &s,
-                             const float *__restrict__ arow, float *orow, double &reward, int64_t *dem) {
+                             const float *__restrict__ arow, float *orow, double &reward, int64_t *dem,
+                             double *irec) {
     const int64_t S = P.cm.Npad;
     const int J = P.J, E = P.E, RL = P.RL;
     const bool leader = gl == 0;
@@ -132,6 +133,18 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, Pcg &
         LV(s.Sr, r) = sale;
         LV(s.U, r) = P.backlog ? fill - sale : 0.0;
     }
+    double *rr = (irec && leader) ? irec + e * (2 * RL + 2 * J + 2 * E) : nullptr;
+    if (rr) {  // step record: S[t, retail], U[t+1, retail], X[t+1], R[t], Y[t+1] (P[t] below)
+        for (int r = 0; r < RL; r++) {
+            rr[r] = LV(s.Sr, r);
+            rr[RL + r] = LV(s.U, r);
+        }
+        for (int j = 0; j < J; j++) rr[2 * RL + j] = LV(s.X, j);
+        for (int k = 0; k < E; k++) {
+            rr[2 * RL + J + k] = LV(s.Rn, k);
+            rr[2 * RL + J + E + k] = LV(s.Y, k);
+        }
+    }
     // 5) profit per main node (:578-613), Python sum() order = adjacency order
     double total = 0.0;
     for (int j = 0; j < J; j++) {
@@ -155,7 +168,9 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, Pcg &
         if (P.is_retail[j])
             for (int q = P.succ_ptr[j]; q < P.succ_ptr[j + 1]; q++)
                 if (P.succ_kind[q] == 1) UP += P.rl_b[P.succ_idx[q]] * LV(s.U, P.succ_idx[q]);
-        total += SR - PC - OC - HC - UP;
+        const double pj = SR - PC - OC - HC - UP;
+        if (rr) rr[2 * RL + J + 2 * E + j] = pj;                // P[t, node]
+        total += pj;
     }
     reward = P.alpha_pow[t] * total;                        // :619
     // obs (:334-413): U[t+1] (RL), X[t+1] (J), then for each link with L>0 in
@@ -233,7 +248,8 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io) {
             } else {
                 double r;
                 tr = net_step_lds(P, e, gl, t, g, s, io.act + oi * P.E, trow, r,
-                                  k == io.K - 1 ? P.cm.info_demand : nullptr);
+                                  k == io.K - 1 ? P.cm.info_demand : nullptr,
+                                  k == io.K - 1 ? (double *)P.cm.info_rec : nullptr);
                 if (leader) {
                     io.rew[oi] = r;
                     io.term[oi] = 0;

@@ -62,7 +62,7 @@ template <class G>
 __device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst (&pc)[G::RL], const double *rhs_l,
                                             int t, double apow, NetSt<G> &s, const float (&act)[G::E],
                                             float *orow, double (&Rn)[G::E], int64_t (&dem)[G::RL],
-                                            double *met) {
+                                            double *met, double *irec) {
     // market demand draws, retail-link order (:536-541)
     double Dd[G::RL];
 #pragma unroll
@@ -123,6 +123,20 @@ __device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst 
         Sr[r] = sale;
         s.U[r] = P.backlog ? fill - sale : 0.0;
     }
+    if (irec) {  // step record: S[t, retail], U[t+1, retail], X[t+1, main] (network_management.py:536-571)
+#pragma unroll
+        for (int r = 0; r < G::RL; r++) {
+            irec[r] = Sr[r];
+            irec[G::RL + r] = s.U[r];
+        }
+#pragma unroll
+        for (int j = 0; j < G::J; j++) irec[2 * G::RL + j] = s.X[j];
+#pragma unroll
+        for (int k = 0; k < G::E; k++) {
+            irec[2 * G::RL + G::J + k] = Rn[k];              // R[t]
+            irec[2 * G::RL + G::J + G::E + k] = s.Y[k];      // Y[t+1]
+        }
+    }
     if (met) {   // evaluate_agent metrics (benchmark_NetInvMgmtLostSalesEnv.py:264-300)
 #pragma unroll
         for (int r = 0; r < G::RL; r++) {
@@ -162,7 +176,9 @@ __device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst 
                 if (G::succ_kind[q] == 1) UP += G::rl_b[G::succ_idx[q] < G::RL ? G::succ_idx[q] : 0] *
                                                 s.U[G::succ_idx[q] < G::RL ? G::succ_idx[q] : 0];
         }
-        total += SR - PC - OC - HC - UP;
+        const double pj = SR - PC - OC - HC - UP;
+        if (irec) irec[2 * G::RL + G::J + 2 * G::E + j] = pj;   // P[t, node]
+        total += pj;
     }
     // obs (:334-413): U[t+1], X[t+1], then per link with L > 0 the fulfilled
     // orders R[t+1-L .. t] oldest first (ages L-1 .. 1, then R[t])
@@ -311,7 +327,9 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
             }
         } else {
             int64_t dem[G::RL];
-            const double r = spec_step<G>(P, pc, rhs_l, t, apow, st, act, trow, Rn, dem, POL ? met : nullptr);
+            double *irec = (valid && kk == K - 1 && P.cm.info_rec)
+                               ? (double *)P.cm.info_rec + e * (2 * G::RL + 2 * G::J + 2 * G::E) : nullptr;
+            const double r = spec_step<G>(P, pc, rhs_l, t, apow, st, act, trow, Rn, dem, POL ? met : nullptr, irec);
             tr = t + 1 >= P.T;
             if (POL) {
                 met[0] += r;                    // episode_reward += reward

@@ -23,7 +23,7 @@ EXPORTS = (
     "invsim_create_invmgmt", "invsim_create_netinvmgmt", "invsim_destroy", "invsim_dims",
     "invsim_set_autoreset", "invsim_seed_range", "invsim_seed_words", "invsim_reset",
     "invsim_step", "invsim_rollout", "invsim_status", "invsim_kernel_variant", "invsim_metrics_dim",
-    "invsim_rollout_policy", "invsim_set_info_demand",
+    "invsim_rollout_policy", "invsim_info_record_dim", "invsim_set_info_record", "invsim_set_info_demand",
     "invsim_state_bytes",
     "invsim_state_field", "invsim_get_state", "invsim_set_state",
 )
@@ -91,6 +91,8 @@ def _declare(lib):
         "invsim_status": ([H, P, I32], C.c_int),
         "invsim_kernel_variant": ([H, P], C.c_int),
         "invsim_metrics_dim": ([H, P], C.c_int),
+        "invsim_info_record_dim": ([H, P], C.c_int),
+        "invsim_set_info_record": ([H, P], C.c_int),
         "invsim_rollout_policy": ([H, I32, P, P, P, P, P, P, P, P], C.c_int),
         "invsim_set_info_demand": ([H, P], C.c_int),
         "invsim_state_bytes": ([H, P], C.c_int),

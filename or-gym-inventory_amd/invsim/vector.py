@@ -64,7 +64,7 @@ class InvSimVectorEnv:
     act_dtype = torch.float32
 
     def __init__(self, num_envs, device=None, autoreset_mode="next_step", global_offset=0,
-                 record_demand=False, copy=True):
+                 record_demand=False, record_info=False, copy=True):
         if not torch.cuda.is_available():
             raise RuntimeError("invsim requires a ROCm GPU (torch.cuda.is_available() is False); "
                                "there is no CPU fallback")
@@ -92,7 +92,35 @@ class InvSimVectorEnv:
                                        device=self.device)
             _capi.check(self._lib.invsim_set_info_demand(self._h, self._demand.data_ptr()),
                         self._h, "set_info_demand")
+        self._rec = None
+        if record_info:
+            d = _capi.C.c_int32()
+            _capi.check(self._lib.invsim_info_record_dim(self._h, _capi.C.byref(d)), self._h, "info_record_dim")
+            if d.value == 0:
+                raise ValueError("record_info: this env family keeps no step record")
+            rdt = torch.int64 if self.family == _capi.INVSIM_INVMGMT else torch.float64
+            self._rec = torch.zeros((self.num_envs, d.value), dtype=rdt, device=self.device)
+            _capi.check(self._lib.invsim_set_info_record(self._h, self._rec.data_ptr()), self._h, "set_info_record")
         self._out = None
+
+    def _record_info(self, info):
+        """Decode the per-step record into the reference's step-info names."""
+        rec = self._rec.clone()
+        if self.family == _capi.INVSIM_INVMGMT:
+            m = (rec.shape[1] - 5) // 2
+            info["sales"] = rec[:, :m]
+            info["unfulfilled"] = rec[:, m:2 * m]
+            f = rec[:, 2 * m:].view(torch.float64)
+            for i, k in enumerate(("period_profit", "revenue", "procurement_cost", "holding_cost", "penalty_cost")):
+                info[k] = f[:, i]
+        else:
+            RL, J, E = len(self.retail_links), len(self.main_nodes), len(self.reorder_links)
+            o = 0
+            for k, w in (("sales", RL), ("unfulfilled", RL), ("inventory", J), ("replenishment", E),
+                         ("pipeline", E), ("profit", J)):
+                info[k] = rec[:, o:o + w]   # S[t], U[t+1] (retail links); X[t+1]; R[t], Y[t+1]; P[t]
+                o += w
+        return info
 
     # -- subclass hooks ------------------------------------------------------
     def _create(self):
@@ -202,6 +230,8 @@ class InvSimVectorEnv:
             info["_final_obs"] = trunc
         if self._demand is not None:
             info["demand"] = self._demand.clone() if self.demand_dim > 1 else self._demand[:, 0].clone()
+        if self._rec is not None:
+            self._record_info(info)
         return obs, rew, term, trunc, info
 
     def rollout(self, actions):
