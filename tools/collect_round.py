@@ -1,0 +1,69 @@
+"""Copy one tools/gpu_round.sh output (gpurun_out/round_TAG) into profiles/ROUND:
+per-workload rocprofv3 kernel stats, the PMC summary JSON (tools/pmc_summary.py)
+and the bench JSON lines, plus a markdown table of the lot.
+
+  python tools/collect_round.py TAG [ROUND=r01]
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {"invmgmt_backlog": "im_run_kernel", "invmgmt_lostsales": "im_run_kernel",
+           "newsvendor": "nv_run_kernel", "net_backlog": "net_spec_kernel"}
+
+
+def last_json(path):
+    if not os.path.exists(path):
+        return None
+    for line in reversed(open(path).read().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    return None
+
+
+def main():
+    tag = sys.argv[1]
+    rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
+    src = os.path.join(ROOT, "gpurun_out", f"round_{tag}")
+    dst = os.path.join(ROOT, "profiles", rnd)
+    os.makedirs(dst, exist_ok=True)
+    rows = []
+    for wl, kern in KERNELS.items():
+        prof = os.path.join(src, f"prof_{wl}")
+        if os.path.isdir(prof):
+            shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"),
+                        os.path.join(dst, f"{wl}_step_kernel_stats.csv"))
+            subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), prof, wl, kern,
+                            os.path.join(dst, f"pmc_{wl}.json")], check=True, capture_output=True)
+        for mode in ("step", "rollout"):
+            b = last_json(os.path.join(src, f"bench_{wl}_{mode}.log"))
+            if b is None:
+                continue
+            with open(os.path.join(dst, f"bench_{wl}_{mode}.json"), "w") as f:
+                json.dump(b, f, indent=1)
+            r = b["roofline"]
+            pmc = os.path.join(dst, f"pmc_{wl}.json")
+            pm = json.load(open(pmc)) if os.path.exists(pmc) and mode == "step" else {}
+            rows.append(f"| {wl} | {mode} | {b['config']['envs_per_gpu']} | {b['value'] / 1e9:.3f} G | "
+                        f"{r['kernel_ms_mean'] * 1e3:.2f} | {r['bytes_per_env_step']:.0f} | {r['achieved']:.0f} | "
+                        f"{r['frac']:.3f} | "
+                        + (f"{pm['rocprof_kernel_ns_mean'] / 1e3:.2f} | {pm['traffic_over_algorithmic']:.2f} |"
+                           if pm else " | |"))
+    d = last_json(os.path.join(src, "bench_default.log"))
+    if d:
+        with open(os.path.join(dst, "bench_default.json"), "w") as f:
+            json.dump(d, f, indent=1)
+    with open(os.path.join(dst, "SUMMARY.md"), "w") as f:
+        f.write(f"# Round {rnd} measurements (gpurun_out/round_{tag}, 1x MI355X)\n\n")
+        f.write("| workload | mode | envs | env-steps/s | kernel µs/launch (events) | B/env-step | "
+                "achieved GB/s | frac of 8 TB/s | rocprof µs (step) | PMC traffic / algorithmic |\n")
+        f.write("|---|---|---|---|---|---|---|---|---|---|\n")
+        f.write("\n".join(rows) + "\n")
+    print(open(os.path.join(dst, "SUMMARY.md")).read())
+
+
+if __name__ == "__main__":
+    main()
