@@ -49,6 +49,16 @@ __device__ __forceinline__ int64_t min_via_f64(int64_t a, int64_t sup) {
     return (int64_t)((x <= y) ? x : y);
 }
 
+// The step's global stores, issued after the obs tile store: gfx9 VMEM stores
+// read their data VGPRs late and vmcnt also counts stores, so a store issued
+// before the tile copy makes every later overwrite of its data registers wait
+// for the store to complete.
+template <int M1>
+struct ImPending {
+    int64_t R[M1], req[M1];
+    int t;
+};
+
 template <int M1, bool BACKLOG>
 struct ImState {
     Pcg g;
@@ -78,7 +88,8 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
                                              ImState<M1, BACKLOG> &s,
                                              const int64_t *__restrict__ arow, int64_t *orow,
                                              const double *rhs, TableStage *ts, double apow, int64_t udem,
-                                             double &reward, int64_t &dem_out, double *met, int64_t *irec) {
+                                             double &reward, int64_t &dem_out, double *met, int64_t *irec,
+                                             ImPending<M1> &pend) {
     const int64_t S = P.cm.Npad;
     const int D = P.lt_max;
     const bool leader = valid && j == 0;   // state writes
@@ -149,9 +160,9 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
     for (int i = 0; i < M1; i++) {
         const int L = P.L[i];
         Icur[i] = wrap_add(s.I[i], L == 0 ? R[i] : arr[i]);
-        if (L > 0 && leader)
-            st_store(P.Rring + (int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e, R[i]);
+        pend.R[i] = R[i];                                           // ring slot t mod L <- R[t] (:267)
     }
+    pend.t = t;
     const int64_t dfill = wrap_add(d, s.B[0]);                      // :284-286
     const int64_t s0 = Icur[0] < dfill ? Icur[0] : dfill;           // :288
     Icur[0] = wrap_sub(Icur[0], s0);
@@ -174,6 +185,7 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
     }
     const double profit = np_sum<double>(M1 + 1, [&](int q) { return term[q]; });
     reward = apow * profit;                                         // :322
+    TPROBE(6);
 #pragma unroll
     for (int i = 0; i < M1; i++) s.I[i] = Icur[i];                  // :326
 #pragma unroll
@@ -215,33 +227,51 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
         if (j == 0) {
 #pragma unroll
             for (int i = 0; i < M1; i++) orow[i] = Icur[i];
-            if (D > 0) {
-#pragma unroll
-                for (int i = 0; i < M1; i++) w[(n - 1) * M1 + i] = req[i];
-            }
         }
         if (D > 0) {
             if (wreg) {
+                // branch-free: the WL = (D-1)*M1 oldest slots get the window or 0,
+                // then the tail slots are cleared before an early-episode newest row
 #pragma unroll
                 for (int u = 0; u < WL; u++) {
                     const int q = j + u * LPE;
-                    if (q < nw) w[q] = wv[u];
+                    if (q < (D - 1) * M1) w[q] = (q < nw) ? wv[u] : 0;
                 }
+                if (n < D)
+                    for (int q = (D - 1) * M1 + j; q < D * M1; q += LPE) w[q] = 0;
             } else {
 #ifndef INVSIM_ABL_NO_WINDOW
                 for (int q = j; q < nw; q += LPE) w[q] = *wsrc(q);
 #endif
+                for (int q = n * M1 + j; q < D * M1; q += LPE) w[q] = 0;
             }
-            for (int q = n * M1 + j; q < D * M1; q += LPE) w[q] = 0;
+        }
+        if (j == 0 && D > 0) {
+#pragma unroll
+            for (int i = 0; i < M1; i++) w[(n - 1) * M1 + i] = req[i];   // newest row last (:380)
         }
     }
-    if (D > 0 && leader) {
-        const int wslot = (int)((uint32_t)t % (uint32_t)D);
 #pragma unroll
-        for (int i = 0; i < M1; i++) st_store(P.alog + ((int64_t)wslot * M1 + i) * S + e, req[i]);  // :268
-    }
+    for (int i = 0; i < M1; i++) pend.req[i] = req[i];              // action_log[t] (:268)
     TPROBE(3);
     return t1 >= P.periods;                                         // :350
+}
+
+template <int M1>
+__device__ __forceinline__ void im_flush_pending(const ImParams &P, const ImPending<M1> &pend, int64_t e) {
+    const int64_t S = P.cm.Npad;
+    const int t = pend.t;
+#pragma unroll
+    for (int i = 0; i < M1; i++) {
+        const int L = P.L[i];
+        if (L > 0) st_store(P.Rring + (int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e, pend.R[i]);
+    }
+    const int D = P.lt_max;
+    if (D > 0) {
+        const int wslot = (int)((uint32_t)t % (uint32_t)D);
+#pragma unroll
+        for (int i = 0; i < M1; i++) st_store(P.alog + ((int64_t)wslot * M1 + i) * S + e, pend.req[i]);
+    }
 }
 
 // BaseStockAgent.get_action (benchmark_InvManagementBacklogEnv.py:152-198): order
@@ -290,6 +320,10 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
     const int O = M1 * (P.lt_max + 1);
     const int64_t oi = (int64_t)k * N + e;
     bool tr = false;
+    bool stepped = false;
+    double rew = 0.0;
+    int64_t dem = 0;
+    ImPending<M1> pend;
     if (!STEP_ONLY && ts) {   // all lanes write the table before the divergent branch
         ts->flush(lane);
         ts = nullptr;
@@ -333,17 +367,15 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
         }
         tr = im_step_regs<M1, BACKLOG, NPD>(P, e, valid, j, t, st, arow, trow, rhs, ts, apow, udem, r, d,
                                             POL ? met : nullptr,
-                                            (valid && leader && k == io.K - 1) ? (int64_t *)P.cm.info_rec : nullptr);
+                                            (valid && leader && k == io.K - 1) ? (int64_t *)P.cm.info_rec : nullptr,
+                                            pend);
+        stepped = true;
         if (POL) {
             met[0] += r;                                            // episode_reward += reward
             met[1] += 1.0;                                          // episode_steps
         }
-        if (valid && leader && (!POL || io.rew)) {
-            out_store(io.rew + oi, r);
-            out_store(io.term + oi, (uint8_t)0);
-            out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
-        }
-        if (valid && leader && k == io.K - 1 && P.cm.info_demand) P.cm.info_demand[e] = d;
+        rew = r;
+        dem = d;
         t += 1;
     }
     wave_lds_sync();
@@ -363,6 +395,16 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
         store_tile<(M1 * 11 * EPW * 8 + 16 * WAVE - 1) / (16 * WAVE)>(tile, io.obs + ((int64_t)k * N + e0) * O,
                                                                      (int64_t)nvalid * O, lane);
 #endif
+    // the step's own stores, after the tile copy (see ImPending)
+    if (stepped && valid && leader) {
+        im_flush_pending<M1>(P, pend, e);
+        if (!POL || io.rew) {
+            out_store(io.rew + oi, rew);
+            out_store(io.term + oi, (uint8_t)0);
+            out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
+        }
+        if (k == io.K - 1 && P.cm.info_demand) P.cm.info_demand[e] = dem;
+    }
     TPROBE(4);
     wave_lds_sync();
 }

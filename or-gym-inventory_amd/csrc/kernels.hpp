@@ -19,7 +19,7 @@ enum { AR_NEXT_STEP = 0, AR_SAME_STEP = 1, AR_DISABLED = 2 };
 // library): lane 0 of wave b writes s_memrealtime (100 MHz) for probe i to
 // g_tbuf[b][i]; probe 7 holds (XCC_ID << 32) | HW_ID.
 #ifdef INVSIM_TIMING
-constexpr int TB_WAVES = 4096, TB_PROBES = 8;
+constexpr int TB_WAVES = 4096, TB_PROBES = 8;   // probe 7: hardware ids
 #define TPROBE(i)                                                                              \
     do {                                                                                       \
         if (threadIdx.x == 0 && blockIdx.x < TB_WAVES)                                         \

@@ -61,6 +61,10 @@ def main():
     for i in range(1, 6):
         d = b[:, i] - b[:, i - 1]
         print(f"{names[i - 1]:>6}->{names[i]:<10}" + " ".join(f"{ns(v):7.0f}" for v in np.percentile(d, [0, 10, 50, 90, 100])))
+    if not args.newsvendor:
+        for a_, b_, nm in ((2, 6, "demand->reward"), (6, 3, "reward->tile")):
+            d = b[:, b_] - b[:, a_]
+            print(f"{nm:<22}" + " ".join(f"{ns(v):7.0f}" for v in np.percentile(d, [0, 10, 50, 90, 100])))
     tot = b[:, 5] - b[:, 0]
     print("wave total       " + " ".join(f"{ns(v):7.0f}" for v in np.percentile(tot, [0, 10, 50, 90, 100])))
     hw = b[:, 7] & 0xFFFFFFFF
