@@ -345,6 +345,7 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
     int64_t o_B = lay.add("B", 8, h->im_backlog ? m : 1, h->Npad);
     int64_t o_R = lay.add("Rring", 8, std::max(sumL, 1), h->Npad);
     int64_t o_A = lay.add("alog", 8, std::max(D * m1, 1), h->Npad);
+    int64_t o_A32 = lay.add("alog32", 4, std::max(D * m1, 1), h->Npad);
     // Generator.integers draws 32-bit halves: the bit generator's buffered half is
     // state (the dist 2-4 kernel variant carries the row; only dist 3 uses it)
     const int64_t o_U32 = (s->dist >= 2 && s->dist <= 4) ? lay.add("u32buf", 8, 1, h->Npad) : -1;
@@ -395,6 +396,7 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
         p.B = at<int64_t>(h, o_B);
         p.Rring = at<int64_t>(h, o_R);
         p.alog = at<int64_t>(h, o_A);
+        p.alog32 = at<uint32_t>(h, o_A32);
         rc = init_period(h, s->periods);
     }
     return finish_create(h, out, rc);

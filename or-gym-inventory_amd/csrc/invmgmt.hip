@@ -14,7 +14,9 @@
 //   B[M1+1]          backlog carried into the period (backlog only)  (:208)
 //   Rring[sum L_i]   fulfilled orders R; stage i keeps its last L_i in a ring,
 //                    slot t mod L_i = R[t-L_i] = this period's arrival (:275)
-//   alog[D][M1]      requested orders (action_log) ring of D = lt_max rows:
+//   alog32[D][Npad][M1] requested orders (action_log) ring of D = lt_max rows, 32-bit,
+//                    an env's row contiguous
+//                    (alog: int64 ring for the rare entries >= 2^32 - 1):
 //                    exactly the observation window (:380)
 //   period (only when not lock-step), PCG64
 // Ring entries older than the episode are masked by the period counter, as the
@@ -33,7 +35,18 @@ __device__ uint64_t g_tbuf[TB_WAVES * TB_PROBES];
 
 // obs-window entries per lane kept in registers: the (lt_max - 1) * M1 entries
 // of lt_max <= 10, capped at 36 (longer windows are copied ring -> LDS directly)
-constexpr int im_wlane(int m1) { return (9 * m1 < 36 ? 9 * m1 : 36 + LPE - 1) / LPE; }
+// Requested orders are >= 0 (np.maximum(action, 0), :250) and, for any sane
+// policy, far below 2^32: the action_log ring keeps 4 bytes per entry, with a
+// sentinel sending the rare wider value to the int64 ring (halves the step's
+// largest read, the observation window)
+constexpr uint32_t IM_WIDE = 0xFFFFFFFFu;
+
+__device__ __forceinline__ int64_t alog_get(const ImParams &P, int64_t idx) {
+    const uint32_t v = P.alog32[idx];
+    return v == IM_WIDE ? P.alog[idx] : (int64_t)v;
+}
+
+constexpr int im_wlane(int m1) { return m1 * (9 < 36 / m1 ? 9 : 36 / m1); }   // whole rows
 
 // numpy int64 array arithmetic wraps around (two's complement)
 __device__ __forceinline__ int64_t wrap_add(int64_t a, int64_t b) {
@@ -113,24 +126,31 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
     const int n = D > 0 ? (t1 < D ? t1 : D) : 0;
     const int nw = n > 0 ? (n - 1) * M1 : 0;
     const int slot0 = D > 0 ? (int)((uint32_t)(t1 - n) % (uint32_t)D) : 0;
-    auto wsrc = [&](int q) -> const int64_t * {
-        const int r = q / M1, i = q - r * M1;
+    // action_log ring layout [slot][env][stage]: one env's row of a slot is M1
+    // contiguous words, so a window row is one vector load (dwordx3 at M1 = 3)
+    auto wrow = [&](int r) -> int64_t {
         int slot = slot0 + r;
         slot = slot >= D ? slot - D : slot;
-        return P.alog + ((int64_t)slot * M1 + i) * S + e;
+        return ((int64_t)slot * S + e) * M1;
+    };
+    auto widx = [&](int q) -> int64_t {
+        const int r = q / M1, i = q - r * M1;
+        return wrow(r) + i;
     };
     constexpr int WL = im_wlane(M1);
     const bool wreg = orow && (D - 1) * M1 <= WL * LPE;   // launch-uniform
-    int64_t wv[WL];
+    uint32_t wv[WL];
 #ifndef INVSIM_ABL_NO_WINDOW
     {   // unconditional (straight-line loads, exact vmcnt waits): entries past nw
         // (start of an episode) re-read the last valid one, or entry 0, always a
         // valid ring row; unused when !wreg
-        const int qmax = nw > 0 ? nw - 1 : 0;
+        static_assert(LPE == 1, "window rows are loaded whole per lane");
+        const int rmax = nw > 0 ? nw / M1 - 1 : 0;   // last valid window row
 #pragma unroll
-        for (int u = 0; u < WL; u++) {
-            const int q = j + u * LPE;
-            wv[u] = *wsrc(q < qmax ? q : qmax);
+        for (int r = 0; r < WL / M1; r++) {
+            const uint32_t *src = P.alog32 + wrow(r < rmax ? r : rmax);
+#pragma unroll
+            for (int i = 0; i < M1; i++) wv[r * M1 + i] = src[i];
         }
     }
 #endif
@@ -232,16 +252,25 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
             if (wreg) {
                 // branch-free: the WL = (D-1)*M1 oldest slots get the window or 0,
                 // then the tail slots are cleared before an early-episode newest row
+                bool wide = false;
 #pragma unroll
                 for (int u = 0; u < WL; u++) {
                     const int q = j + u * LPE;
-                    if (q < (D - 1) * M1) w[q] = (q < nw) ? wv[u] : 0;
+                    if (q < (D - 1) * M1) w[q] = (q < nw) ? (int64_t)wv[u] : 0;
+                    wide |= (q < nw) && wv[u] == IM_WIDE;
+                }
+                if (wide) {   // rare: entries >= 2^32 - 1 come from the int64 ring
+#pragma unroll
+                    for (int u = 0; u < WL; u++) {
+                        const int q = j + u * LPE;
+                        if (q < nw && wv[u] == IM_WIDE) w[q] = P.alog[widx(q)];
+                    }
                 }
                 if (n < D)
                     for (int q = (D - 1) * M1 + j; q < D * M1; q += LPE) w[q] = 0;
             } else {
 #ifndef INVSIM_ABL_NO_WINDOW
-                for (int q = j; q < nw; q += LPE) w[q] = *wsrc(q);
+                for (int q = j; q < nw; q += LPE) w[q] = alog_get(P, widx(q));
 #endif
                 for (int q = n * M1 + j; q < D * M1; q += LPE) w[q] = 0;
             }
@@ -270,7 +299,12 @@ __device__ __forceinline__ void im_flush_pending(const ImParams &P, const ImPend
     if (D > 0) {
         const int wslot = (int)((uint32_t)t % (uint32_t)D);
 #pragma unroll
-        for (int i = 0; i < M1; i++) st_store(P.alog + ((int64_t)wslot * M1 + i) * S + e, pend.req[i]);
+        for (int i = 0; i < M1; i++) {
+            const int64_t idx = ((int64_t)wslot * S + e) * M1 + i;
+            const bool wide = pend.req[i] >= (int64_t)IM_WIDE;
+            st_store(P.alog32 + idx, wide ? IM_WIDE : (uint32_t)pend.req[i]);
+            if (wide) st_store(P.alog + idx, pend.req[i]);
+        }
     }
 }
 
@@ -292,7 +326,7 @@ __device__ __forceinline__ void im_base_stock(const ImParams &P, const PolicyIO 
             for (int a = 1; a <= L; a++) {
                 const int tau = t - a;
                 if (tau >= 0)
-                    pipe = wrap_add(pipe, P.alog[((int64_t)((uint32_t)tau % (uint32_t)D) * M1 + i) * S + e]);
+                    pipe = wrap_add(pipe, alog_get(P, ((int64_t)((uint32_t)tau % (uint32_t)D) * S + e) * M1 + i));
             }
             pos = wrap_add(pos, pipe);
         }

@@ -83,7 +83,9 @@ struct ImParams {
     int64_t *I;                  // [M1][Npad]   on-hand inventory I[t]
     int64_t *B;                  // [M1+1][Npad] backlog B[t] (backlog mode only)
     int64_t *Rring;              // [sum L][Npad] fulfilled orders R, ring per stage
-    int64_t *alog;               // [D][M1][Npad] requested orders (action_log), ring
+    uint32_t *alog32;            // [D][Npad][M1] requested orders (action_log) ring, 32-bit;
+                                 //   IM_WIDE = the value is >= 2^32 - 1 and lives in alog
+    int64_t *alog;               // [D][Npad][M1] int64 ring, written only for IM_WIDE entries
 };
 
 // ---------------------------------------------------------------- NetInvMgmt

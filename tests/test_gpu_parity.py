@@ -448,3 +448,24 @@ def test_invmgmt_integers_buffer_is_state(gpu):
     e3 = mk()
     e3.reset(seed=5)
     assert torch.equal(e1.step(a)[4]["demand"], e3.step(a)[4]["demand"])
+
+
+def test_invmgmt_action_log_32bit_boundary(gpu, oracle):
+    """The action_log ring is 32-bit with a sentinel for values >= 2^32 - 1:
+    requested orders at and around the boundary round-trip exactly (obs window,
+    BaseStock pipeline) against the int64 oracle."""
+    from invsim import InvManagementBacklogEnv
+    n = 256
+    env = InvManagementBacklogEnv(n, device=gpu, c=(2**40, 2**40, 2**40))
+    orc = oracle.OracleInvMgmt(n, c=(2**40, 2**40, 2**40))
+    orc.seed(range(9, 9 + n))
+    orc.reset()
+    env.reset(seed=9)
+    vals = np.array([0, 1, 2**31 - 1, 2**31, 2**32 - 2, 2**32 - 1, 2**32, 2**33 + 5, 2**40, 7], np.int64)
+    rng = np.random.default_rng(4)
+    for s in range(30):
+        a = vals[rng.integers(0, len(vals), size=(n, 3))]
+        o, r, te, tr, info = env.step(torch.from_numpy(a).to(gpu))
+        e_obs, e_rew, e_tr = orc.step(a)
+        assert np.array_equal(o.cpu().numpy(), e_obs), f"obs step {s}"
+        _assert_reward(r.cpu().numpy(), e_rew, f"step {s}")
