@@ -242,7 +242,9 @@ int invsim_info_record_dim(const invsim_handle *h, int32_t *dim);
 int invsim_set_info_record(invsim_handle *h, void *record);
 
 /* Checkpoint / debug: the full device state as one opaque blob of state_bytes,
- * plus a field directory (name, byte offset, element size, rows) for tests. */
+ * plus a field directory for tests: name, byte offset, element size, rows and
+ * row_stride: > 0 rows of row_stride elements ([rows][row_stride]); < 0 a
+ * record per env ([-row_stride][rows]); 0 another layout (opaque). */
 int invsim_state_bytes(const invsim_handle *h, int64_t *bytes);
 int invsim_state_field(const invsim_handle *h, int32_t idx, char name[32], int64_t *offset,
                        int32_t *elem_bytes, int32_t *rows, int64_t *row_stride);

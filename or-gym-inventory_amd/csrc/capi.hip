@@ -23,7 +23,8 @@ struct Field {
     std::string name;
     int64_t offset;   // bytes from arena start
     int32_t elem;     // element bytes
-    int32_t rows;
+    int32_t rows;     // rows, or record width
+    int32_t kind;     // 0: [rows][Npad]; 1: record [Npad][rows]; 2: other (opaque)
 };
 
 }  // namespace
@@ -85,9 +86,9 @@ int hip_fail(invsim_handle *h, hipError_t e, const char *what) {
 struct Layout {
     std::vector<Field> f;
     int64_t bytes = 0;
-    int64_t add(const char *name, int32_t elem, int32_t rows, int64_t npad) {
+    int64_t add(const char *name, int32_t elem, int32_t rows, int64_t npad, int32_t kind = 0) {
         bytes = (bytes + 255) / 256 * 256;
-        Field x{name, bytes, elem, rows};
+        Field x{name, bytes, elem, rows, kind};
         f.push_back(x);
         bytes += (int64_t)elem * rows * npad;
         return x.offset;
@@ -344,8 +345,8 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
     int64_t o_I = lay.add("I", 8, m1, h->Npad);
     int64_t o_B = lay.add("B", 8, h->im_backlog ? m : 1, h->Npad);
     int64_t o_R = lay.add("Rring", 8, std::max(sumL, 1), h->Npad);
-    int64_t o_A = lay.add("alog", 8, std::max(D * m1, 1), h->Npad);
-    int64_t o_A32 = lay.add("alog32", 4, std::max(D * m1, 1), h->Npad);
+    int64_t o_A = lay.add("alog", 8, std::max(D * m1, 1), h->Npad, 2);      // [D][Npad][m1]
+    int64_t o_A32 = lay.add("alog32", 4, std::max(D * m1, 1), h->Npad, 2);  // [D][Npad][m1]
     // Generator.integers draws 32-bit halves: the bit generator's buffered half is
     // state (the dist 2-4 kernel variant carries the row; only dist 3 uses it)
     const int64_t o_U32 = (s->dist >= 2 && s->dist <= 4) ? lay.add("u32buf", 8, 1, h->Npad) : -1;
@@ -823,7 +824,8 @@ int invsim_state_field(const invsim_handle *h, int32_t idx, char name[32], int64
     if (offset) *offset = f.offset;
     if (elem_bytes) *elem_bytes = f.elem;
     if (rows) *rows = f.rows;
-    if (row_stride) *row_stride = (f.name == "status") ? 1 : h->Npad;
+    // > 0: [rows][row_stride]; < 0: record layout [-row_stride][rows]; 0: other layout
+    if (row_stride) *row_stride = (f.name == "status") ? 1 : f.kind == 1 ? -h->Npad : f.kind == 2 ? 0 : h->Npad;
     return INVSIM_OK;
 }
 

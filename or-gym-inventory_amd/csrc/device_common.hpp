@@ -296,6 +296,9 @@ __device__ __forceinline__ T np_sum(int n, Get get) {
 }
 
 // ---------------------------------------------------------------- RNG state I/O
+// PCG64 per env as four SoA rows (state_hi, state_lo, inc_hi, inc_lo): a
+// wave's load of a row is 512 contiguous bytes (a 32-byte record per env was
+// measured 1 % slower on the InvMgmt step: twice the cache lines per load)
 struct RngSoA {
     uint64_t *hi, *lo, *inc_hi, *inc_lo;
     __device__ __forceinline__ Pcg load(int64_t e) const {

@@ -304,9 +304,13 @@ class InvSimVectorEnv:
                                               _capi.C.byref(rows), _capi.C.byref(stride))
             if rc != 0:
                 break
-            n = rows.value * stride.value * eb.value
-            raw = blob[off.value: off.value + n].view(dt[eb.value]).view(rows.value, stride.value)
-            out[name.value.decode()] = raw[:, : self.num_envs] if stride.value > 1 else raw
+            r_, st_ = rows.value, stride.value
+            if st_ > 0:     # [rows][stride]
+                raw = blob[off.value: off.value + r_ * st_ * eb.value].view(dt[eb.value]).view(r_, st_)
+                out[name.value.decode()] = raw[:, : self.num_envs] if st_ > 1 else raw
+            elif st_ < 0:   # record layout [Npad][rows] -> [rows, N] view
+                raw = blob[off.value: off.value + r_ * -st_ * eb.value].view(dt[eb.value]).view(-st_, r_)
+                out[name.value.decode()] = raw[: self.num_envs].t()
             i += 1
         return out
 
