@@ -566,7 +566,232 @@ im_reset_kernel(ImParams P, const uint8_t *__restrict__ mask, int64_t *__restric
     }
 }
 
+// Cross-wave LDS handoff inside a workgroup: orders LDS traffic only (an
+// __syncthreads() would also drain each wave's outstanding global loads and
+// stores, s_waitcnt vmcnt(0), before the s_barrier)
+__device__ __forceinline__ void wg_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Single lock-step step (invsim_step, K = 1, t_u < periods, no SAME_STEP reset
+// in this step) with the work of 64 envs split over two waves of one
+// workgroup, so one wave's demand draw overlaps the other's global loads:
+//   wave 0 (demand)   RHS table, PCG64 (+ 32-bit buffer), demand draw, the
+//                     observation window rows t+1-n .. t-1 of the action_log
+//                     ring into the LDS tile, PCG64 store
+//   wave 1 (dynamics) actions, arrivals, I, B; the demand-independent part of
+//                     the dynamics, then (after the handoff of d through LDS)
+//                     sales, backlog, reward, the tile's inventory and newest
+//                     action row, and the state / output stores
+// Both waves then store half of the observation tile.  Same arithmetic, in
+// the same order, as im_step_regs (inventory_management.py:224-352).
+template <int M1, bool BACKLOG, bool NPD>
+__global__ void __launch_bounds__(2 * WAVE)
+im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io) {
+    extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const bool demand_wave = threadIdx.x < WAVE;
+    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e = e0 + lane;
+    const int64_t N = P.cm.N;
+    const bool valid = e < N;
+    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
+    const int D = P.lt_max;
+    const int O = M1 * (D + 1);
+    const int64_t S = P.cm.Npad;
+    int64_t *trow = im_tile + (int64_t)lane * O;
+    int64_t *w = trow + M1;
+    double *rhs_l = reinterpret_cast<double *>(im_tile + (int64_t)WAVE * O);
+    int64_t *dsh = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);
+    const int t1 = t + 1;
+    const int n = D > 0 ? (t1 < D ? t1 : D) : 0;                    // window rows incl. the newest
+    const int nw = n > 0 ? (n - 1) * M1 : 0;
+    // the tile halves each wave stores (16-byte aligned: an even int64 count)
+    const int64_t tcount = (int64_t)nvalid * O;
+    const int64_t thalf = ((tcount / 2) + 1) & ~(int64_t)1;
+    if (demand_wave) {
+        TableStage ts;
+        ts.dst = rhs_l;
+        {
+            const bool has_tab = P.pc.nk > 0 && P.dist == 1;
+            const double *tsrc = has_tab ? P.rhs : P.alpha_pow;    // any valid pointer
+            const int qm = has_tab ? P.pc.nk - 1 : 0;
+#pragma unroll
+            for (int u = 0; u < TableStage::NT; u++) ts.v[u] = tsrc[min(lane + u * WAVE, qm)];
+        }
+        Pcg g = P.cm.rng.load(valid ? e : N - 1);   // padded lanes: the last env's stream
+        uint64_t u32 = NPD ? P.cm.u32buf[valid ? e : N - 1] : 0;
+        const int64_t udem = P.user_D[t];
+        // window rows t+1-n .. t-1 (:380), loaded whole (see im_step_regs)
+        const int slot0 = D > 0 ? (int)((uint32_t)(t1 - n) % (uint32_t)D) : 0;
+        auto wrow = [&](int r) -> int64_t {
+            int slot = slot0 + r;
+            slot = slot >= D ? slot - D : slot;
+            return ((int64_t)slot * S + e) * M1;
+        };
+        constexpr int WL = im_wlane(M1);
+        const bool wreg = (D - 1) * M1 <= WL;   // launch-uniform
+        uint32_t wv[WL];
+        {
+            const int rmax = nw > 0 ? nw / M1 - 1 : 0;
+#pragma unroll
+            for (int r = 0; r < WL / M1; r++) {
+                const uint32_t *src = P.alog32 + wrow(r < rmax ? r : rmax);
+#pragma unroll
+                for (int i = 0; i < M1; i++) wv[r * M1 + i] = src[i];
+            }
+        }
+        ts.flush(lane);
+        int64_t d = NPD ? np_demand(g, u32, P.nd) : (P.dist == 5) ? udem : env_poisson(g, P.pc, rhs_l);
+        if (d < 0) d = 0;
+        dsh[lane] = d;
+        if (D > 0) {   // the window part of the obs rows; the newest row is the dynamics wave's
+            if (wreg) {
+                bool wide = false;
+#pragma unroll
+                for (int u = 0; u < WL; u++) {
+                    if (u < (D - 1) * M1) w[u] = (u < nw) ? (int64_t)wv[u] : 0;
+                    wide |= (u < nw) && wv[u] == IM_WIDE;
+                }
+                if (wide) {
+#pragma unroll
+                    for (int u = 0; u < WL; u++)
+                        if (u < nw && wv[u] == IM_WIDE) w[u] = P.alog[wrow(u / M1) + u % M1];
+                }
+                if (n < D)
+                    for (int q = (D - 1) * M1; q < D * M1; q++) w[q] = 0;
+            } else {
+                for (int q = 0; q < nw; q++) w[q] = alog_get(P, wrow(q / M1) + q % M1);
+                for (int q = n * M1; q < D * M1; q++) w[q] = 0;
+            }
+        }
+        wg_lds_sync();   // d and the window rows -> dynamics wave
+        if (valid) {
+            P.cm.rng.store_state(e, g);
+            if (NPD) P.cm.u32buf[e] = u32;
+        }
+        wg_lds_sync();   // tile complete
+        store_tile<(M1 * 11 * WAVE * 8 / 2 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + e0 * O,
+                                                                          thalf < tcount ? thalf : tcount, lane);
+        return;
+    }
+    // ---- dynamics wave
+    const double apow = P.alpha_pow[t];
+    const int64_t *arow = io.act + (valid ? e : N - 1) * M1;
+    int64_t req[M1], arr[M1], I[M1], B[M1 + 1];
+#pragma unroll
+    for (int i = 0; i < M1; i++) req[i] = arow[i];
+#pragma unroll
+    for (int i = 0; i < M1; i++) {                                  // arrivals R[t-L_i] (:271-277)
+        const int L = P.L[i];
+        const int row = L > 0 ? P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L) : 0;
+        arr[i] = P.Rring[(int64_t)row * S + e];
+        if (!(L > 0 && t >= L)) arr[i] = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < M1; i++) I[i] = P.I[i * S + e];
+#pragma unroll
+    for (int q = 0; q <= M1; q++) B[q] = BACKLOG ? P.B[q * S + e] : 0;
+    int64_t ordreq[M1], R[M1], Icur[M1];
+#pragma unroll
+    for (int i = 0; i < M1; i++) req[i] = req[i] > 0 ? req[i] : 0;  // :250
+#pragma unroll
+    for (int i = 0; i < M1; i++) {
+        ordreq[i] = wrap_add(req[i], B[i + 1]);                     // :253-255
+        const int64_t r = ordreq[i] < P.c[i] ? ordreq[i] : P.c[i];  // :263
+        R[i] = (i + 1 < M1) ? min_via_f64(r, I[i + 1]) : (int64_t)(double)r;   // :260-265
+    }
+#pragma unroll
+    for (int i = 0; i < M1; i++) Icur[i] = wrap_add(I[i], P.L[i] == 0 ? R[i] : arr[i]);
+#pragma unroll
+    for (int i = 1; i < M1; i++) Icur[i] = wrap_sub(Icur[i], R[i]); // :300 (reference quirk, kept)
+    int64_t Sv[M1 + 1], U[M1 + 1];
+#pragma unroll
+    for (int i = 0; i < M1; i++) {
+        Sv[i + 1] = R[i];                                           // :295
+        U[i + 1] = wrap_sub(ordreq[i], R[i]);                       // :304
+    }
+    wg_lds_sync();   // d from the demand wave
+    const int64_t d = dsh[lane];
+    const int64_t dfill = wrap_add(d, B[0]);                        // :284-286
+    const int64_t s0 = Icur[0] < dfill ? Icur[0] : dfill;           // :288
+    Icur[0] = wrap_sub(Icur[0], s0);
+    Sv[0] = s0;
+    U[0] = wrap_sub(dfill, s0);                                     // :303
+    double term[M1 + 1];                                            // :315-321
+#pragma unroll
+    for (int q = 0; q <= M1; q++) {
+        const double Sj = (double)Sv[q];
+        const int64_t inv = (q < M1) ? Icur[q] : 0;
+        const double hold = P.hc[q] * (double)(inv > 0 ? inv : 0);
+        term[q] = ((P.up[q] * Sj - P.uc[q] * Sj) - hold) - P.kc[q] * (double)U[q];
+    }
+    const double profit = np_sum<double>(M1 + 1, [&](int q) { return term[q]; });
+    const double reward = apow * profit;                            // :322
+#pragma unroll
+    for (int i = 0; i < M1; i++) trow[i] = Icur[i];                 // obs (:354-391)
+    if (D > 0) {
+#pragma unroll
+        for (int i = 0; i < M1; i++) w[(n - 1) * M1 + i] = req[i];  // newest row last (:380)
+    }
+    wg_lds_sync();   // tile complete
+    {
+        const int64_t h = thalf < tcount ? thalf : tcount;
+        if (tcount > h)
+            store_tile<(M1 * 11 * WAVE * 8 / 2 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile + h, io.obs + e0 * O + h,
+                                                                              tcount - h, lane);
+    }
+    if (!valid) return;
+    if (P.cm.info_rec) {   // step info (:334-345), as im_step_regs
+        constexpr int W = 2 * (M1 + 1) + 5;
+        int64_t *rr = (int64_t *)P.cm.info_rec + e * W;
+#pragma unroll
+        for (int q = 0; q <= M1; q++) {
+            rr[q] = Sv[q];
+            rr[M1 + 1 + q] = U[q];
+        }
+        const double rev = np_sum<double>(M1 + 1, [&](int q) { return P.up[q] * (double)Sv[q]; });
+        const double pro = np_sum<double>(M1 + 1, [&](int q) { return P.uc[q] * (double)Sv[q]; });
+        const double hol = np_sum<double>(M1 + 1, [&](int q) {
+            const int64_t inv = (q < M1) ? Icur[q] : 0;
+            return P.hc[q] * (double)(inv > 0 ? inv : 0);
+        });
+        const double pen = np_sum<double>(M1 + 1, [&](int q) { return P.kc[q] * (double)U[q]; });
+        rr[2 * (M1 + 1) + 0] = __double_as_longlong(profit);
+        rr[2 * (M1 + 1) + 1] = __double_as_longlong(rev);
+        rr[2 * (M1 + 1) + 2] = __double_as_longlong(pro);
+        rr[2 * (M1 + 1) + 3] = __double_as_longlong(hol);
+        rr[2 * (M1 + 1) + 4] = __double_as_longlong(pen);
+    }
+    ImPending<M1> pend;
+#pragma unroll
+    for (int i = 0; i < M1; i++) {
+        pend.R[i] = R[i];                                           // ring slot t mod L <- R[t] (:267)
+        pend.req[i] = req[i];                                       // action_log[t] (:268)
+    }
+    pend.t = t;
+    im_flush_pending<M1>(P, pend, e);
+    out_store(io.rew + e, reward);
+    out_store(io.term + e, (uint8_t)0);
+    out_store(io.trunc + e, (uint8_t)(t1 >= P.periods ? 1 : 0));   // :350
+    if (P.cm.info_demand) P.cm.info_demand[e] = d;
+#pragma unroll
+    for (int i = 0; i < M1; i++) st_store(P.I + i * S + e, Icur[i]);   // :326
+    if (BACKLOG) {
+#pragma unroll
+        for (int q = 0; q <= M1; q++) st_store(P.B + q * S + e, U[q]);   // :307-312
+    }
+}
+
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// INVSIM_IM_SPLIT=0 keeps single steps on the one-wave kernel (A/B measurements)
+inline bool im_split_enabled() {
+    const char *s = getenv("INVSIM_IM_SPLIT");
+    return !(s && s[0] == '0');
+}
 
 }  // namespace
 
@@ -591,7 +816,22 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
     const bool npd = p.dist >= 2 && p.dist <= 4;
-#define K_(M, B, TU, ONE, POL)                                                                          \
+    if (!pol && io.K == 1 && t_u >= 0 && t_u < p.periods && io.obs &&
+        !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.periods) && im_split_enabled()) {
+        const size_t lds2 = lds + WAVE * sizeof(int64_t);
+        const dim3 block2(2 * WAVE);
+#define S_(M, B)                                                                                        \
+    do {                                                                                                \
+        if (npd)                                                                                        \
+            hipLaunchKernelGGL((im_split_kernel<M, B, true>), grid, block2, lds2, s, p, t_u, io);       \
+        else                                                                                            \
+            hipLaunchKernelGGL((im_split_kernel<M, B, false>), grid, block2, lds2, s, p, t_u, io);      \
+    } while (0)
+        IM_DISPATCH(M1, backlog, S_)
+#undef S_
+        return hipGetLastError();
+    }
+#define K_(M, B, TU, ONE, POL)                                                                         \
     do {                                                                                                \
         if (npd)                                                                                        \
             hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL, true>), grid, block, lds, s, p, t_u, io, pv);  \

@@ -469,3 +469,48 @@ def test_invmgmt_action_log_32bit_boundary(gpu, oracle):
         e_obs, e_rew, e_tr = orc.step(a)
         assert np.array_equal(o.cpu().numpy(), e_obs), f"obs step {s}"
         _assert_reward(r.cpu().numpy(), e_rew, f"step {s}")
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(cls="InvManagementBacklogEnv", kw={}),
+    dict(cls="InvManagementLostSalesEnv", kw={}),
+    dict(cls="InvManagementBacklogEnv", kw=dict(L=(3, 14, 2), I0=(50, 60, 70), c=(80, 90, 100))),   # window > registers
+    dict(cls="InvManagementBacklogEnv", kw=dict(dist=2, dist_param={"n": 400, "p": 0.05})),
+    dict(cls="InvManagementBacklogEnv", kw=dict(dist=3, dist_param={"low": 0, "high": 40})),
+    dict(cls="InvManagementBacklogEnv", kw=dict(dist=5, user_D=list(range(3, 33)))),
+    dict(cls="InvManagementBacklogEnv", kw=dict(L=(0, 2, 1), dist_param={"mu": 4})),             # mult sampler, L = 0
+    dict(cls="InvManagementBacklogEnv", kw=dict(I0=(10, 20, 30, 40), r=(15, 10, 7, 5, 3), k=(0.1, 0.08, 0.06, 0.04, 0.02),
+                                                h=(0.15, 0.1, 0.05, 0.03), c=(100, 200, 230, 250), L=(2, 3, 4, 5))),
+])
+@pytest.mark.parametrize("autoreset", ["next_step", "same_step"])
+def test_invmgmt_split_kernel_equals_one_wave(gpu, cfg, autoreset, monkeypatch):
+    """Single lock-step steps run on the two-wave kernel (demand wave +
+    dynamics wave, im_split_kernel); INVSIM_IM_SPLIT=0 keeps them on the
+    one-wave kernel.  Trajectories, info records and state are bit-identical."""
+    import invsim
+    cls = getattr(invsim, cfg["cls"])
+    n, K = 1000, 65                      # padded lanes; two episodes and the resets between them
+    envs = [cls(n, device=gpu, autoreset_mode=autoreset, record_demand=True, record_info=True, **cfg["kw"])
+            for _ in range(2)]
+    m1 = envs[0].action_dim
+    g = torch.Generator(device=gpu).manual_seed(3)
+    a = torch.randint(-5, 120, (K, n, m1), device=gpu, dtype=torch.int64, generator=g)
+    for env in envs:
+        env.reset(seed=77)
+    for k in range(K):
+        out = []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_IM_SPLIT", "1" if i == 0 else "0")
+            o, r, te, tr, info = env.step(a[k])
+            out.append((o.clone(), r.clone(), te.clone(), tr.clone(),
+                        {key: v.clone() for key, v in info.items() if torch.is_tensor(v)}))
+        for x, y in zip(out[0][:4], out[1][:4]):
+            assert torch.equal(x, y), k
+        for key in out[0][4]:
+            if key == "final_obs":
+                msk = out[0][4]["_final_obs"]
+                assert torch.equal(out[0][4][key][msk], out[1][4][key][msk]), k
+            else:
+                assert torch.equal(out[0][4][key], out[1][4][key]), (key, k)
+    monkeypatch.delenv("INVSIM_IM_SPLIT")
+    assert torch.equal(envs[0].get_state(), envs[1].get_state())
