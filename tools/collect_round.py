@@ -11,7 +11,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"invmgmt_backlog": "im_run_kernel", "invmgmt_lostsales": "im_run_kernel",
+KERNELS = {"invmgmt_backlog": "im_split_kernel", "invmgmt_lostsales": "im_split_kernel",
            "newsvendor": "nv_run_kernel", "net_backlog": "net_spec_kernel"}
 
 

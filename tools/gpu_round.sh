@@ -20,7 +20,7 @@ WLS="invmgmt_backlog invmgmt_lostsales newsvendor net_backlog"
 for part in $PARTS; do
   case $part in
   tests)
-    run timeout -k 10 420 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1
+    run timeout -k 10 480 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
     tail -2 $OUT/pytest_gpu.log ;;
   bench)
     run timeout -k 10 180 python bench.py > $OUT/bench_default.log 2>&1
