@@ -41,6 +41,9 @@ struct invsim_handle {
     char *arena = nullptr;      // state (get/set_state blob)
     int64_t arena_bytes = 0;
     char *tables = nullptr;     // read-only tables (not part of the state blob)
+    void *scratch = nullptr;    // caches derived from the state (not part of the blob)
+    bool im_ahead = false;      // InvMgmt demand lookahead cache (ImParams::ahead) is valid
+    int im_slot = 0;            //   ... in this slot
     std::vector<Field> fields;
     Common cm{};
     NvParams nv{};
@@ -222,6 +225,7 @@ void invsim_destroy(invsim_handle *h) {
     DeviceGuard g(h->device);
     if (h->arena) (void)hipFree(h->arena);
     if (h->tables) (void)hipFree(h->tables);
+    if (h->scratch) (void)hipFree(h->scratch);
     delete h;
 }
 
@@ -398,7 +402,13 @@ int invsim_create_invmgmt(const invsim_invmgmt_spec *s, int64_t n, int32_t devic
         p.Rring = at<int64_t>(h, o_R);
         p.alog = at<int64_t>(h, o_A);
         p.alog32 = at<uint32_t>(h, o_A32);
-        rc = init_period(h, s->periods);
+        p.ahead = nullptr;
+        if (s->dist >= 1 && s->dist <= 4) {   // demand lookahead cache: 2 slots x 4 rows x Npad u64
+            hipError_t e = hipMalloc(&h->scratch, (size_t)(2 * 4 * h->Npad * sizeof(uint64_t)));
+            if (e != hipSuccess) rc = fail(h, INVSIM_ENOMEM, "hipMalloc(lookahead cache)");
+            else p.ahead = static_cast<uint64_t *>(h->scratch);
+        }
+        if (rc == INVSIM_OK) rc = init_period(h, s->periods);
     }
     return finish_create(h, out, rc);
 }
@@ -627,6 +637,7 @@ int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int6
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (first < 0) return fail(h, INVSIM_EINVAL, "first_index must be >= 0");
     DeviceGuard g(h->device);
+    h->im_ahead = false;   // the lookahead cache follows the old streams
     hipError_t e = seed_range_launch(h->cm, base_lo, base_hi, first, mask, (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_range launch");
 }
@@ -635,6 +646,7 @@ int invsim_seed_words(invsim_handle *h, const uint32_t *words, const int32_t *nw
                       const uint8_t *mask, void *stream) {
     if (!h || (!words && h->N) || (!nwords && h->N)) return fail(h, INVSIM_EINVAL, "null argument");
     DeviceGuard g(h->device);
+    h->im_ahead = false;
     hipError_t e = seed_words_launch(h->cm, words, nwords, mask, (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_words launch");
 }
@@ -696,7 +708,7 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         case INVSIM_INVMGMT: {
             StepIO<int64_t, int64_t> io{K, (const int64_t *)actions, (int64_t *)obs, reward, terminated, truncated,
                                         (int64_t *)final_obs};
-            e = im_run_launch(h->im, h->im_m1, h->im_backlog, t_u, pol, io, s);
+            e = im_run_launch(h->im, h->im_m1, h->im_backlog, t_u, pol, io, h->im_ahead, h->im_slot, s);
             break;
         }
         case INVSIM_NETINVMGMT: {
@@ -707,7 +719,10 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         }
         default: return fail(h, INVSIM_EINVAL, "bad handle family");
     }
-    if (e != hipSuccess) return hip_fail(h, e, "step launch");
+    if (e != hipSuccess) {
+        h->im_ahead = false;
+        return hip_fail(h, e, "step launch");
+    }
     if (h->t_known)
         for (int k = 0; k < K; k++) h->t_cur = next_period(h->t_cur, h->horizon, h->cm.autoreset, h->past_ok);
     return INVSIM_OK;
@@ -846,6 +861,7 @@ int invsim_set_state(invsim_handle *h, const void *src, void *stream) {
                                   (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(h, e, "set_state");
     h->t_known = false;  // periods now come from the blob
+    h->im_ahead = false;
     return INVSIM_OK;
 }
 

@@ -577,33 +577,93 @@ __device__ __forceinline__ void wg_lds_sync() {
 
 // Single lock-step step (invsim_step, K = 1, t_u < periods, no SAME_STEP reset
 // in this step) with the work of 64 envs split over two waves of one
-// workgroup, so one wave's demand draw overlaps the other's global loads:
-//   wave 0 (demand)   RHS table, PCG64 (+ 32-bit buffer), demand draw, the
-//                     observation window rows t+1-n .. t-1 of the action_log
-//                     ring into the LDS tile, PCG64 store
+// workgroup:
+//   wave 0 (window)   the observation window rows t+1-n .. t-1 of the action_log
+//                     ring into the LDS tile, and this step's demand d
 //   wave 1 (dynamics) actions, arrivals, I, B; the demand-independent part of
 //                     the dynamics, then (after the handoff of d through LDS)
 //                     sales, backlog, reward, the tile's inventory and newest
 //                     action row, and the state / output stores
 // Both waves then store half of the observation tile.  Same arithmetic, in
 // the same order, as im_step_regs (inventory_management.py:224-352).
-template <int M1, bool BACKLOG, bool NPD>
+//
+// Demand lookahead (P.ahead: two slots of [state hi, state lo, demand, 32-bit
+// buffer] x Npad, alternating per launch).  The demand is a function of the
+// env's generator stream only, so each launch also draws the NEXT step's
+// demand.  AHEAD (slot `cur` holds every env's state one draw past the
+// committed one, and that draw): wave 0 just loads d, and `gla` extra
+// workgroups at the front of the grid (128 envs each, no barriers) commit slot
+// cur's state to cm.rng, draw the next demand and write it to slot cur ^ 1 -- so
+// the Poisson chain (~2.5 us) runs beside the step instead of before it.
+// !AHEAD (first step after a seed / set_state / other kernel): wave 0 draws d
+// inline from cm.rng, commits, then draws the lookahead into slot cur ^ 1.
+// Either way every stream is consumed in the reference's order and cm.rng
+// holds exactly the state after this step's draw.
+template <int M1, bool BACKLOG, bool NPD, bool AHEAD>
 __global__ void __launch_bounds__(2 * WAVE)
-im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io) {
+im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int gla) {
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    double *rhs_l = reinterpret_cast<double *>(im_tile + (int64_t)WAVE * M1 * (P.lt_max + 1));
+    uint64_t *Acur = P.ahead ? P.ahead + (int64_t)cur * 4 * S : nullptr;
+    uint64_t *Anxt = P.ahead ? P.ahead + (int64_t)(cur ^ 1) * 4 * S : nullptr;
+    const int64_t udem = P.user_D[t];
+    auto stage_table = [&](int lane) {
+        TableStage ts;
+        ts.dst = rhs_l;
+        const bool has_tab = P.pc.nk > 0 && P.dist == 1;
+        const double *tsrc = has_tab ? P.rhs : P.alpha_pow;    // any valid pointer
+        const int qm = has_tab ? P.pc.nk - 1 : 0;
+#pragma unroll
+        for (int u = 0; u < TableStage::NT; u++) ts.v[u] = tsrc[min(lane + u * WAVE, qm)];
+        return ts;
+    };
+    auto draw = [&](Pcg &g, uint64_t &u32) -> int64_t {
+#ifdef INVSIM_ABL_NO_POISSON  // profiling ablation build only (wrong results)
+        int64_t x = 20 + (int64_t)(g.lo & 3);
+        g.next64();
+#else
+        int64_t x = NPD ? np_demand(g, u32, P.nd) : (P.dist == 5) ? udem : env_poisson(g, P.pc, rhs_l);
+#endif
+        return x < 0 ? 0 : x;
+    };
+    if (AHEAD && (int)blockIdx.x < gla) {   // ---- lookahead workgroup: 128 envs, one per lane
+        const int64_t e = (int64_t)blockIdx.x * (2 * WAVE) + threadIdx.x;
+        const bool valid = e < N;
+        const int64_t ee = valid ? e : N - 1;
+        TableStage ts = stage_table((int)(threadIdx.x & (WAVE - 1)));
+        Pcg g;
+        g.hi = Acur[ee];
+        g.lo = Acur[S + ee];
+        g.inc_hi = P.cm.rng.inc_hi[ee];
+        g.inc_lo = P.cm.rng.inc_lo[ee];
+        uint64_t u32 = NPD ? Acur[3 * S + ee] : 0;
+        ts.flush((int)(threadIdx.x & (WAVE - 1)));   // each wave writes the whole (identical) table
+        if (valid) {                                  // committed: after this step's draw
+            st_store(P.cm.rng.hi + e, g.hi);
+            st_store(P.cm.rng.lo + e, g.lo);
+            if (NPD) st_store(P.cm.u32buf + e, u32);
+        }
+        const int64_t dn = draw(g, u32);
+        if (valid) {
+            st_store(Anxt + e, g.hi);
+            st_store(Anxt + S + e, g.lo);
+            st_store(Anxt + 2 * S + e, (uint64_t)dn);
+            if (NPD) st_store(Anxt + 3 * S + e, u32);
+        }
+        return;
+    }
     const int lane = threadIdx.x & (WAVE - 1);
     const bool demand_wave = threadIdx.x < WAVE;
-    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e0 = (int64_t)(blockIdx.x - (AHEAD ? gla : 0)) * WAVE;
     const int64_t e = e0 + lane;
-    const int64_t N = P.cm.N;
     const bool valid = e < N;
     const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
     const int D = P.lt_max;
     const int O = M1 * (D + 1);
-    const int64_t S = P.cm.Npad;
     int64_t *trow = im_tile + (int64_t)lane * O;
     int64_t *w = trow + M1;
-    double *rhs_l = reinterpret_cast<double *>(im_tile + (int64_t)WAVE * O);
     int64_t *dsh = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);
     const int t1 = t + 1;
     const int n = D > 0 ? (t1 < D ? t1 : D) : 0;                    // window rows incl. the newest
@@ -612,18 +672,18 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io) {
     const int64_t tcount = (int64_t)nvalid * O;
     const int64_t thalf = ((tcount / 2) + 1) & ~(int64_t)1;
     if (demand_wave) {
+        const int64_t ee = valid ? e : N - 1;        // padded lanes: the last env's stream
         TableStage ts;
-        ts.dst = rhs_l;
-        {
-            const bool has_tab = P.pc.nk > 0 && P.dist == 1;
-            const double *tsrc = has_tab ? P.rhs : P.alpha_pow;    // any valid pointer
-            const int qm = has_tab ? P.pc.nk - 1 : 0;
-#pragma unroll
-            for (int u = 0; u < TableStage::NT; u++) ts.v[u] = tsrc[min(lane + u * WAVE, qm)];
+        Pcg g;
+        uint64_t u32 = 0;
+        int64_t d = 0;
+        if (AHEAD) {
+            d = (int64_t)Acur[2 * S + ee];
+        } else {
+            ts = stage_table(lane);
+            g = P.cm.rng.load(ee);
+            if (NPD) u32 = P.cm.u32buf[ee];
         }
-        Pcg g = P.cm.rng.load(valid ? e : N - 1);   // padded lanes: the last env's stream
-        uint64_t u32 = NPD ? P.cm.u32buf[valid ? e : N - 1] : 0;
-        const int64_t udem = P.user_D[t];
         // window rows t+1-n .. t-1 (:380), loaded whole (see im_step_regs)
         const int slot0 = D > 0 ? (int)((uint32_t)(t1 - n) % (uint32_t)D) : 0;
         auto wrow = [&](int r) -> int64_t {
@@ -643,9 +703,10 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io) {
                 for (int i = 0; i < M1; i++) wv[r * M1 + i] = src[i];
             }
         }
-        ts.flush(lane);
-        int64_t d = NPD ? np_demand(g, u32, P.nd) : (P.dist == 5) ? udem : env_poisson(g, P.pc, rhs_l);
-        if (d < 0) d = 0;
+        if (!AHEAD) {
+            ts.flush(lane);
+            d = draw(g, u32);
+        }
         dsh[lane] = d;
         if (D > 0) {   // the window part of the obs rows; the newest row is the dynamics wave's
             if (wreg) {
@@ -668,13 +729,22 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io) {
             }
         }
         wg_lds_sync();   // d and the window rows -> dynamics wave
-        if (valid) {
+        if (!AHEAD && valid) {   // committed generator state: after this step's draw
             P.cm.rng.store_state(e, g);
             if (NPD) P.cm.u32buf[e] = u32;
         }
         wg_lds_sync();   // tile complete
         store_tile<(M1 * 11 * WAVE * 8 / 2 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + e0 * O,
                                                                           thalf < tcount ? thalf : tcount, lane);
+        if (!AHEAD && Anxt) {    // lookahead after an inline draw (first step after invalidation)
+            const int64_t dn = draw(g, u32);
+            if (valid) {
+                st_store(Anxt + e, g.hi);
+                st_store(Anxt + S + e, g.lo);
+                st_store(Anxt + 2 * S + e, (uint64_t)dn);
+                if (NPD) st_store(Anxt + 3 * S + e, u32);
+            }
+        }
         return;
     }
     // ---- dynamics wave
@@ -793,6 +863,12 @@ inline bool im_split_enabled() {
     return !(s && s[0] == '0');
 }
 
+// INVSIM_IM_AHEAD=0 turns the demand lookahead off (A/B measurements)
+inline bool im_ahead_enabled() {
+    const char *s = getenv("INVSIM_IM_AHEAD");
+    return !(s && s[0] == '0');
+}
+
 }  // namespace
 
 #define IM_DISPATCH(M1V, BL, LAUNCH)                                   \
@@ -809,7 +885,7 @@ inline bool im_split_enabled() {
     }
 
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
-                         const StepIO<int64_t, int64_t> &io, hipStream_t s) {
+                         const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = (size_t)EPW * M1 * (p.lt_max + 1) * sizeof(int64_t) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
@@ -820,17 +896,35 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
         !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.periods) && im_split_enabled()) {
         const size_t lds2 = lds + WAVE * sizeof(int64_t);
         const dim3 block2(2 * WAVE);
+        ImParams q = p;
+        if (!im_ahead_enabled()) q.ahead = nullptr;
+        const bool hit = ahead && q.ahead;
+        const int gla = hit ? (int)grid_for(p.cm.N, 2 * WAVE) : 0;   // lookahead workgroups
+        const dim3 grid2(grid.x + gla);
+        const int cur = slot;
 #define S_(M, B)                                                                                        \
     do {                                                                                                \
-        if (npd)                                                                                        \
-            hipLaunchKernelGGL((im_split_kernel<M, B, true>), grid, block2, lds2, s, p, t_u, io);       \
-        else                                                                                            \
-            hipLaunchKernelGGL((im_split_kernel<M, B, false>), grid, block2, lds2, s, p, t_u, io);      \
+        if (npd) {                                                                                      \
+            if (hit) hipLaunchKernelGGL((im_split_kernel<M, B, true, true>), grid2, block2, lds2, s, q, t_u, io, cur, gla);  \
+            else hipLaunchKernelGGL((im_split_kernel<M, B, true, false>), grid2, block2, lds2, s, q, t_u, io, cur, gla);     \
+        } else {                                                                                        \
+            if (hit) hipLaunchKernelGGL((im_split_kernel<M, B, false, true>), grid2, block2, lds2, s, q, t_u, io, cur, gla); \
+            else hipLaunchKernelGGL((im_split_kernel<M, B, false, false>), grid2, block2, lds2, s, q, t_u, io, cur, gla);    \
+        }                                                                                               \
     } while (0)
         IM_DISPATCH(M1, backlog, S_)
 #undef S_
+        if (q.ahead) {                // every env drew its next demand into slot cur ^ 1
+            ahead = true;
+            slot ^= 1;
+        } else {
+            ahead = false;
+        }
         return hipGetLastError();
     }
+    // the one-wave kernel draws from the committed state: the cache is stale
+    // after it, unless this launch is the lock-step autoreset (no draw)
+    if (!(!pol && io.K == 1 && t_u >= p.periods)) ahead = false;
 #define K_(M, B, TU, ONE, POL)                                                                         \
     do {                                                                                                \
         if (npd)                                                                                        \

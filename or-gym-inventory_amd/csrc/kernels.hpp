@@ -86,6 +86,12 @@ struct ImParams {
     uint32_t *alog32;            // [D][Npad][M1] requested orders (action_log) ring, 32-bit;
                                  //   IM_WIDE = the value is >= 2^32 - 1 and lives in alog
     int64_t *alog;               // [D][Npad][M1] int64 ring, written only for IM_WIDE entries
+    // demand lookahead cache (dist 1-4; not part of the state blob): two slots
+    // of rows [state hi, state lo, next demand, 32-bit buffer] x Npad = the env's
+    // PCG64 one draw past the committed state in cm.rng, and that draw.  Valid
+    // only while the host says so (invsim_handle::im_ahead, im_slot); the
+    // committed state stays exact.
+    uint64_t *ahead;
 };
 
 // ---------------------------------------------------------------- NetInvMgmt
@@ -276,8 +282,10 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
 
 hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_t *mask,
                            int64_t *obs, hipStream_t s);
+// ahead: in = lookahead slot `slot` holds every env's next demand; out = the
+// slot (updated) does now
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
-                         const StepIO<int64_t, int64_t> &io, hipStream_t s);
+                         const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s);
 
 // Compile-time specialised NetInvMgmt kernels for the reference's own graphs
 // (netspec.hip): which built-in topology a spec equals, and its launcher.

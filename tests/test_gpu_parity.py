@@ -514,3 +514,65 @@ def test_invmgmt_split_kernel_equals_one_wave(gpu, cfg, autoreset, monkeypatch):
                 assert torch.equal(out[0][4][key], out[1][4][key]), (key, k)
     monkeypatch.delenv("INVSIM_IM_SPLIT")
     assert torch.equal(envs[0].get_state(), envs[1].get_state())
+
+
+@pytest.mark.parametrize("kw", [{}, dict(dist=3, dist_param={"low": 0, "high": 40}),
+                                dict(dist=2, dist_param={"n": 400, "p": 0.05}), dict(dist_param={"mu": 4})])
+def test_invmgmt_demand_lookahead_mixed_calls(gpu, kw, monkeypatch):
+    """Split steps draw the NEXT step's demand into a lookahead cache while the
+    committed generator state stays exact.  Every other path (rollout, policy
+    rollout, re-seed, set_state, masked reset, same-step autoreset, episode
+    boundaries) must leave each env's stream exactly where a cache-free run
+    (INVSIM_IM_AHEAD=0) leaves it: outputs, demands and state blobs identical."""
+    import invsim
+    from invsim.policies import BaseStockAgent
+    n = 777
+    envs = [invsim.InvManagementBacklogEnv(n, device=gpu, periods=9, record_demand=True, **kw) for _ in range(2)]
+    g = torch.Generator(device=gpu).manual_seed(5)
+    A = torch.randint(-5, 150, (200, n, 3), device=gpu, dtype=torch.int64, generator=g)
+    pos = [0]
+
+    def both(fn):
+        outs = []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_IM_AHEAD", "1" if i == 0 else "0")
+            outs.append(fn(env))
+        return outs
+
+    def steps(k):
+        for _ in range(k):
+            a = A[pos[0] % 200]
+            pos[0] += 1
+            o = both(lambda env: [x.clone() if torch.is_tensor(x) else x for x in env.step(a)[:4]]
+                     + [env._demand.clone()])
+            for x, y in zip(o[0], o[1]):
+                assert torch.equal(x, y), pos[0]
+
+    def same_state():
+        s = both(lambda env: env.get_state().clone())
+        assert torch.equal(s[0], s[1]), pos[0]
+
+    both(lambda env: env.reset(seed=21))
+    steps(5)
+    same_state()
+    o = both(lambda env: env.rollout(A[:3]))                 # one-wave kernel after a lookahead
+    assert all(torch.equal(x, y) for x, y in zip(o[0], o[1]))
+    steps(4)                                                 # crosses the horizon (NEXT_STEP reset)
+    ck = both(lambda env: env.get_state().clone())
+    steps(3)
+    both(lambda env: env.reset(seed=22))                    # re-seed invalidates the cache
+    steps(2)
+    both(lambda env: env.set_state(ck[0].clone()))          # back to the checkpoint
+    steps(1)                                                 # per-env periods: one-wave kernel
+    both(lambda env: env.reset())
+    steps(4)
+    m = both(lambda env: env.rollout_policy(BaseStockAgent(), 2, obs=True))
+    assert all(torch.equal(m[0][k], m[1][k]) for k in m[0])
+    steps(3)
+    mask = torch.zeros(n, dtype=torch.bool, device=gpu)
+    mask[::5] = True
+    both(lambda env: env.reset(options={"reset_mask": mask}))
+    steps(3)
+    both(lambda env: env.reset())
+    steps(12)
+    same_state()
