@@ -632,11 +632,20 @@ int invsim_set_info_demand(invsim_handle *h, int64_t *demand) {
     return INVSIM_OK;
 }
 
+// InvMgmt: bring cm.rng up to date from the lookahead cache (the cache stays valid)
+static int im_commit(invsim_handle *h, hipStream_t s) {
+    if (h->family != INVSIM_INVMGMT || !h->im_ahead) return INVSIM_OK;
+    hipError_t e = im_commit_launch(h->im, h->im_slot, s);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "rng commit");
+}
+
 int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int64_t first,
                       const uint8_t *mask, void *stream) {
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (first < 0) return fail(h, INVSIM_EINVAL, "first_index must be >= 0");
     DeviceGuard g(h->device);
+    int rc = im_commit(h, (hipStream_t)stream);   // a masked seed keeps the other streams
+    if (rc != INVSIM_OK) return rc;
     h->im_ahead = false;   // the lookahead cache follows the old streams
     hipError_t e = seed_range_launch(h->cm, base_lo, base_hi, first, mask, (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_range launch");
@@ -646,6 +655,8 @@ int invsim_seed_words(invsim_handle *h, const uint32_t *words, const int32_t *nw
                       const uint8_t *mask, void *stream) {
     if (!h || (!words && h->N) || (!nwords && h->N)) return fail(h, INVSIM_EINVAL, "null argument");
     DeviceGuard g(h->device);
+    int rc = im_commit(h, (hipStream_t)stream);
+    if (rc != INVSIM_OK) return rc;
     h->im_ahead = false;
     hipError_t e = seed_words_launch(h->cm, words, nwords, mask, (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_words launch");
@@ -848,6 +859,7 @@ int invsim_get_state(invsim_handle *h, void *dst, void *stream) {
     if (!h || !dst) return fail(h, INVSIM_EINVAL, "null argument");
     DeviceGuard g(h->device);
     int rc = materialize_period(h, (hipStream_t)stream);  // the blob carries per-env periods
+    if (rc == INVSIM_OK) rc = im_commit(h, (hipStream_t)stream);   // and the committed PCG64 states
     if (rc != INVSIM_OK) return rc;
     hipError_t e = hipMemcpyAsync(dst, h->arena, (size_t)h->arena_bytes, hipMemcpyDeviceToDevice,
                                   (hipStream_t)stream);

@@ -592,16 +592,19 @@ __device__ __forceinline__ void wg_lds_sync() {
 // env's generator stream only, so each launch also draws the NEXT step's
 // demand.  AHEAD (slot `cur` holds every env's state one draw past the
 // committed one, and that draw): wave 0 just loads d, and `gla` extra
-// workgroups at the front of the grid (128 envs each, no barriers) commit slot
-// cur's state to cm.rng, draw the next demand and write it to slot cur ^ 1 -- so
-// the Poisson chain (~2.5 us) runs beside the step instead of before it.
+// workgroups at the front of the grid (128 envs each, no barriers) draw the
+// next demand from slot cur's state and write it to slot cur ^ 1 -- so the
+// Poisson chain (~2.5 us) runs beside the step instead of before it.
 // !AHEAD (first step after a seed / set_state / other kernel): wave 0 draws d
-// inline from cm.rng, commits, then draws the lookahead into slot cur ^ 1.
-// Either way every stream is consumed in the reference's order and cm.rng
-// holds exactly the state after this step's draw.
+// inline from cm.rng, stores that state to slot cur, then draws the lookahead
+// into slot cur ^ 1.  Either way every stream is consumed in the reference's
+// order.  The committed state (after this step's draw) is left in slot cur,
+// which the host flips to `cur ^ 1` of the new current slot; cm.rng is brought
+// up to date from it (im_commit_kernel) only before something reads it: another
+// kernel, get_state, a masked seed.
 template <int M1, bool BACKLOG, bool NPD, bool AHEAD>
 __global__ void __launch_bounds__(2 * WAVE)
-im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int gla) {
+im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0, int gla) {
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
     const int64_t N = P.cm.N;
     const int64_t S = P.cm.Npad;
@@ -628,8 +631,9 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int gla
 #endif
         return x < 0 ? 0 : x;
     };
-    if (AHEAD && (int)blockIdx.x < gla) {   // ---- lookahead workgroup: 128 envs, one per lane
-        const int64_t e = (int64_t)blockIdx.x * (2 * WAVE) + threadIdx.x;
+    const int bid = (int)blockIdx.x;
+    if (AHEAD && bid >= la0 && bid < la0 + gla) {   // ---- lookahead workgroup: 128 envs, one per lane
+        const int64_t e = (int64_t)(bid - la0) * (2 * WAVE) + threadIdx.x;
         const bool valid = e < N;
         const int64_t ee = valid ? e : N - 1;
         TableStage ts = stage_table((int)(threadIdx.x & (WAVE - 1)));
@@ -640,11 +644,7 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int gla
         g.inc_lo = P.cm.rng.inc_lo[ee];
         uint64_t u32 = NPD ? Acur[3 * S + ee] : 0;
         ts.flush((int)(threadIdx.x & (WAVE - 1)));   // each wave writes the whole (identical) table
-        if (valid) {                                  // committed: after this step's draw
-            st_store(P.cm.rng.hi + e, g.hi);
-            st_store(P.cm.rng.lo + e, g.lo);
-            if (NPD) st_store(P.cm.u32buf + e, u32);
-        }
+        // slot cur keeps this state: the committed one once the slots flip
         const int64_t dn = draw(g, u32);
         if (valid) {
             st_store(Anxt + e, g.hi);
@@ -656,7 +656,7 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int gla
     }
     const int lane = threadIdx.x & (WAVE - 1);
     const bool demand_wave = threadIdx.x < WAVE;
-    const int64_t e0 = (int64_t)(blockIdx.x - (AHEAD ? gla : 0)) * WAVE;
+    const int64_t e0 = (int64_t)(AHEAD && bid >= la0 ? bid - gla : bid) * WAVE;
     const int64_t e = e0 + lane;
     const bool valid = e < N;
     const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
@@ -730,8 +730,14 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int gla
         }
         wg_lds_sync();   // d and the window rows -> dynamics wave
         if (!AHEAD && valid) {   // committed generator state: after this step's draw
-            P.cm.rng.store_state(e, g);
-            if (NPD) P.cm.u32buf[e] = u32;
+            if (Acur) {          // into slot cur (the committed slot once the slots flip)
+                st_store(Acur + e, g.hi);
+                st_store(Acur + S + e, g.lo);
+                if (NPD) st_store(Acur + 3 * S + e, u32);
+            } else {
+                P.cm.rng.store_state(e, g);
+                if (NPD) P.cm.u32buf[e] = u32;
+            }
         }
         wg_lds_sync();   // tile complete
         store_tile<(M1 * 11 * WAVE * 8 / 2 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + e0 * O,
@@ -855,12 +861,29 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int gla
     }
 }
 
+// cm.rng <- the committed slot of the lookahead cache (see im_split_kernel)
+__global__ void __launch_bounds__(256) im_commit_kernel(ImParams P, int slot) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P.cm.N) return;
+    const int64_t S = P.cm.Npad;
+    const uint64_t *A = P.ahead + (int64_t)slot * 4 * S;
+    P.cm.rng.hi[e] = A[e];
+    P.cm.rng.lo[e] = A[S + e];
+    if (P.cm.u32buf) P.cm.u32buf[e] = A[3 * S + e];
+}
+
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 // INVSIM_IM_SPLIT=0 keeps single steps on the one-wave kernel (A/B measurements)
 inline bool im_split_enabled() {
     const char *s = getenv("INVSIM_IM_SPLIT");
     return !(s && s[0] == '0');
+}
+
+// INVSIM_IM_LA_LAST=1 puts the lookahead workgroups at the end of the grid (A/B)
+inline bool im_la_last() {
+    const char *s = getenv("INVSIM_IM_LA_LAST");
+    return s && s[0] == '1';
 }
 
 // INVSIM_IM_AHEAD=0 turns the demand lookahead off (A/B measurements)
@@ -898,18 +921,24 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
         const dim3 block2(2 * WAVE);
         ImParams q = p;
         if (!im_ahead_enabled()) q.ahead = nullptr;
+        if (ahead && !q.ahead) {      // lookahead switched off: commit, then draw inline
+            const hipError_t ce = im_commit_launch(p, slot, s);
+            ahead = false;
+            if (ce != hipSuccess) return ce;
+        }
         const bool hit = ahead && q.ahead;
         const int gla = hit ? (int)grid_for(p.cm.N, 2 * WAVE) : 0;   // lookahead workgroups
         const dim3 grid2(grid.x + gla);
         const int cur = slot;
+        const int la0 = im_la_last() ? (int)grid.x : 0;   // lookahead workgroups first (default) or last
 #define S_(M, B)                                                                                        \
     do {                                                                                                \
         if (npd) {                                                                                      \
-            if (hit) hipLaunchKernelGGL((im_split_kernel<M, B, true, true>), grid2, block2, lds2, s, q, t_u, io, cur, gla);  \
-            else hipLaunchKernelGGL((im_split_kernel<M, B, true, false>), grid2, block2, lds2, s, q, t_u, io, cur, gla);     \
+            if (hit) hipLaunchKernelGGL((im_split_kernel<M, B, true, true>), grid2, block2, lds2, s, q, t_u, io, cur, la0, gla);  \
+            else hipLaunchKernelGGL((im_split_kernel<M, B, true, false>), grid2, block2, lds2, s, q, t_u, io, cur, la0, gla);     \
         } else {                                                                                        \
-            if (hit) hipLaunchKernelGGL((im_split_kernel<M, B, false, true>), grid2, block2, lds2, s, q, t_u, io, cur, gla); \
-            else hipLaunchKernelGGL((im_split_kernel<M, B, false, false>), grid2, block2, lds2, s, q, t_u, io, cur, gla);    \
+            if (hit) hipLaunchKernelGGL((im_split_kernel<M, B, false, true>), grid2, block2, lds2, s, q, t_u, io, cur, la0, gla); \
+            else hipLaunchKernelGGL((im_split_kernel<M, B, false, false>), grid2, block2, lds2, s, q, t_u, io, cur, la0, gla);    \
         }                                                                                               \
     } while (0)
         IM_DISPATCH(M1, backlog, S_)
@@ -922,9 +951,14 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
         }
         return hipGetLastError();
     }
-    // the one-wave kernel draws from the committed state: the cache is stale
-    // after it, unless this launch is the lock-step autoreset (no draw)
-    if (!(!pol && io.K == 1 && t_u >= p.periods)) ahead = false;
+    // the one-wave kernel draws from the committed state (brought into cm.rng
+    // first): the cache is stale after it, unless this launch is the lock-step
+    // autoreset (no draw)
+    if (!(!pol && io.K == 1 && t_u >= p.periods) && ahead) {
+        const hipError_t ce = im_commit_launch(p, slot, s);
+        ahead = false;
+        if (ce != hipSuccess) return ce;
+    }
 #define K_(M, B, TU, ONE, POL)                                                                         \
     do {                                                                                                \
         if (npd)                                                                                        \
@@ -948,6 +982,12 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     IM_DISPATCH(M1, backlog, L_)
 #undef L_
 #undef K_
+    return hipGetLastError();
+}
+
+hipError_t im_commit_launch(const ImParams &p, int slot, hipStream_t s) {
+    if (p.cm.N == 0 || !p.ahead) return hipSuccess;
+    hipLaunchKernelGGL(im_commit_kernel, dim3(grid_for(p.cm.N, 256)), dim3(256), 0, s, p, slot ^ 1);
     return hipGetLastError();
 }
 

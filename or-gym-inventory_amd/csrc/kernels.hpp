@@ -286,6 +286,9 @@ hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_
 // slot (updated) does now
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
                          const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s);
+// cm.rng <- the committed generator state held by the lookahead cache (whose
+// current slot is `slot`); needed before anything reads cm.rng while it is valid
+hipError_t im_commit_launch(const ImParams &p, int slot, hipStream_t s);
 
 // Compile-time specialised NetInvMgmt kernels for the reference's own graphs
 // (netspec.hip): which built-in topology a spec equals, and its launcher.
