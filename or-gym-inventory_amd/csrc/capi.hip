@@ -42,8 +42,8 @@ struct invsim_handle {
     int64_t arena_bytes = 0;
     char *tables = nullptr;     // read-only tables (not part of the state blob)
     void *scratch = nullptr;    // caches derived from the state (not part of the blob)
-    bool im_ahead = false;      // InvMgmt demand lookahead cache (ImParams::ahead) is valid
-    int im_slot = 0;            //   ... in this slot
+    bool la_valid = false;      // demand lookahead cache (Im/NvParams::ahead) is valid
+    int la_slot = 0;            //   ... with this current slot
     std::vector<Field> fields;
     Common cm{};
     NvParams nv{};
@@ -275,8 +275,14 @@ int invsim_create_newsvendor(const invsim_newsvendor_spec *spec, int64_t n, int3
         p.mu_max = spec->mu_max;
         p.par = at<double>(h, o_par);
         p.pipe = at<float>(h, o_pipe);
+        p.ahead = nullptr;
+        {   // demand lookahead cache: 2 slots x 3 rows x Npad u64
+            hipError_t e = hipMalloc(&h->scratch, (size_t)(2 * 3 * h->Npad * sizeof(uint64_t)));
+            if (e != hipSuccess) rc = fail(h, INVSIM_ENOMEM, "hipMalloc(lookahead cache)");
+            else p.ahead = static_cast<uint64_t *>(h->scratch);
+        }
         h->past_ok = true;
-        rc = init_period(h, std::max(spec->step_limit, 0));
+        if (rc == INVSIM_OK) rc = init_period(h, std::max(spec->step_limit, 0));
     }
     return finish_create(h, out, rc);
 }
@@ -632,10 +638,12 @@ int invsim_set_info_demand(invsim_handle *h, int64_t *demand) {
     return INVSIM_OK;
 }
 
-// InvMgmt: bring cm.rng up to date from the lookahead cache (the cache stays valid)
-static int im_commit(invsim_handle *h, hipStream_t s) {
-    if (h->family != INVSIM_INVMGMT || !h->im_ahead) return INVSIM_OK;
-    hipError_t e = im_commit_launch(h->im, h->im_slot, s);
+// bring cm.rng up to date from the demand lookahead cache (the cache stays valid)
+static int commit_rng(invsim_handle *h, hipStream_t s) {
+    if (!h->la_valid) return INVSIM_OK;
+    hipError_t e = hipSuccess;
+    if (h->family == INVSIM_INVMGMT) e = im_commit_launch(h->im, h->la_slot, s);
+    else if (h->family == INVSIM_NEWSVENDOR) e = nv_commit_launch(h->nv, h->la_slot, s);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "rng commit");
 }
 
@@ -644,9 +652,9 @@ int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int6
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (first < 0) return fail(h, INVSIM_EINVAL, "first_index must be >= 0");
     DeviceGuard g(h->device);
-    int rc = im_commit(h, (hipStream_t)stream);   // a masked seed keeps the other streams
+    int rc = commit_rng(h, (hipStream_t)stream);   // a masked seed keeps the other streams
     if (rc != INVSIM_OK) return rc;
-    h->im_ahead = false;   // the lookahead cache follows the old streams
+    h->la_valid = false;   // the lookahead cache follows the old streams
     hipError_t e = seed_range_launch(h->cm, base_lo, base_hi, first, mask, (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_range launch");
 }
@@ -655,9 +663,9 @@ int invsim_seed_words(invsim_handle *h, const uint32_t *words, const int32_t *nw
                       const uint8_t *mask, void *stream) {
     if (!h || (!words && h->N) || (!nwords && h->N)) return fail(h, INVSIM_EINVAL, "null argument");
     DeviceGuard g(h->device);
-    int rc = im_commit(h, (hipStream_t)stream);
+    int rc = commit_rng(h, (hipStream_t)stream);
     if (rc != INVSIM_OK) return rc;
-    h->im_ahead = false;
+    h->la_valid = false;
     hipError_t e = seed_words_launch(h->cm, words, nwords, mask, (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_words launch");
 }
@@ -676,6 +684,11 @@ int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream)
     if (mask) {
         int rc = materialize_period(h, s);
         if (rc != INVSIM_OK) return rc;
+    }
+    if (h->family == INVSIM_NEWSVENDOR) {   // its reset draws from cm.rng
+        int rc = commit_rng(h, s);
+        if (rc != INVSIM_OK) return rc;
+        h->la_valid = false;
     }
     hipError_t e = hipSuccess;
     switch (h->family) {
@@ -713,13 +726,13 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
     switch (h->family) {
         case INVSIM_NEWSVENDOR: {
             StepIO<float, float> io{K, (const float *)actions, (float *)obs, reward, terminated, truncated, (float *)final_obs};
-            e = nv_run_launch(h->nv, t_u, pol, io, s);
+            e = nv_run_launch(h->nv, t_u, pol, io, h->la_valid, h->la_slot, s);
             break;
         }
         case INVSIM_INVMGMT: {
             StepIO<int64_t, int64_t> io{K, (const int64_t *)actions, (int64_t *)obs, reward, terminated, truncated,
                                         (int64_t *)final_obs};
-            e = im_run_launch(h->im, h->im_m1, h->im_backlog, t_u, pol, io, h->im_ahead, h->im_slot, s);
+            e = im_run_launch(h->im, h->im_m1, h->im_backlog, t_u, pol, io, h->la_valid, h->la_slot, s);
             break;
         }
         case INVSIM_NETINVMGMT: {
@@ -731,7 +744,7 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         default: return fail(h, INVSIM_EINVAL, "bad handle family");
     }
     if (e != hipSuccess) {
-        h->im_ahead = false;
+        h->la_valid = false;
         return hip_fail(h, e, "step launch");
     }
     if (h->t_known)
@@ -859,7 +872,7 @@ int invsim_get_state(invsim_handle *h, void *dst, void *stream) {
     if (!h || !dst) return fail(h, INVSIM_EINVAL, "null argument");
     DeviceGuard g(h->device);
     int rc = materialize_period(h, (hipStream_t)stream);  // the blob carries per-env periods
-    if (rc == INVSIM_OK) rc = im_commit(h, (hipStream_t)stream);   // and the committed PCG64 states
+    if (rc == INVSIM_OK) rc = commit_rng(h, (hipStream_t)stream);   // and the committed PCG64 states
     if (rc != INVSIM_OK) return rc;
     hipError_t e = hipMemcpyAsync(dst, h->arena, (size_t)h->arena_bytes, hipMemcpyDeviceToDevice,
                                   (hipStream_t)stream);
@@ -873,7 +886,7 @@ int invsim_set_state(invsim_handle *h, const void *src, void *stream) {
                                   (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(h, e, "set_state");
     h->t_known = false;  // periods now come from the blob
-    h->im_ahead = false;
+    h->la_valid = false;
     return INVSIM_OK;
 }
 

@@ -61,6 +61,9 @@ struct NvParams {
     double *par;         // [5][Npad]  price, cost, h, k, mu  (Python floats)
     const double *lgtab; // [RHS_LDS_MAX] loggam(k + 1), host (numpy's formula)
     float *pipe;         // [L][Npad]  order ring, slot = step index mod L
+    // demand lookahead cache (not part of the state blob): two slots of rows
+    // [state hi, state lo, next demand] x Npad (nv_step1_kernel)
+    uint64_t *ahead;
 };
 
 // ---------------------------------------------------------------- InvMgmt
@@ -277,8 +280,10 @@ hipError_t seed_words_launch(const Common &cm, const uint32_t *words, const int3
 hipError_t period_fill_launch(const Common &cm, int32_t t, hipStream_t s);
 
 hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, hipStream_t s);
+// ahead / slot: the demand lookahead cache state, as for im_run_launch
 hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
-                         hipStream_t s);
+                         bool &ahead, int &slot, hipStream_t s);
+hipError_t nv_commit_launch(const NvParams &p, int slot, hipStream_t s);
 
 hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_t *mask,
                            int64_t *obs, hipStream_t s);

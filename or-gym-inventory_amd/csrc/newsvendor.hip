@@ -124,7 +124,7 @@ __device__ __forceinline__ float nv_order_up_to(const NvParams &P, const PolicyI
 template <int LT>
 __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool valid, int sc, NvState<LT> &s,
                                              float action, float *orow, const double *lg_l, TableStage *ts,
-                                             double &reward, int64_t *dem) {
+                                             double &reward, int64_t *dem, int64_t dpre = -1) {
     const int64_t S = P.cm.Npad;
     const int L = (LT >= 0) ? LT : P.L;
     const int base = (L > 0) ? (int)((uint32_t)(sc + 1) % (uint32_t)L) : 0;  // slot of position 0
@@ -136,7 +136,8 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
     };
     if (ts) ts->flush((int)threadIdx.x);
     TPROBE(1);
-    const int64_t d = env_poisson_dyn(s.g, s.par[4], lg_l, RHS_LDS_MAX);  // :146
+    // :146 (dpre >= 0: drawn by the previous launch's lookahead, nv_step1_kernel)
+    const int64_t d = dpre >= 0 ? dpre : env_poisson_dyn(s.g, s.par[4], lg_l, RHS_LDS_MAX);
     TPROBE(2);
     const Tv ZERO = tv(0.0, K_PY);
     const Tv oq = tv(np_clip((double)action, 0.0, P.max_order), K_F64);    // :131-132
@@ -294,6 +295,142 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     TPROBE(5);
 }
 
+// Single lock-step step (invsim_step: K = 1, t_u < step_limit, no policy, not a
+// SAME_STEP done step) with the demand lookahead.  The demand of a step is
+// Poisson(mu) of the env's own stream, and mu is fixed for the episode, so the
+// launch of step t can already draw step t+1's demand (PRODUCE, i.e. t+1 <
+// step_limit: the step after the last one is a reset, which draws uniforms).
+// P.ahead: two slots of rows [state hi, state lo, demand] x Npad, alternating.
+//   HIT (slot cur holds each env's state one draw past the committed one and
+//        that draw): the step workgroups load d; `gla` workgroups at the front
+//        of the grid draw the next demand from slot cur's state into slot cur^1
+//        (PRODUCE) -- the per-env-rate Poisson chain runs beside the step -- or
+//        copy slot cur's state to cm.rng (!PRODUCE: the cache ends here).
+//   !HIT && PRODUCE: the step draws d inline from cm.rng, leaves the state in
+//        slot cur, then draws the lookahead into slot cur^1.
+// After a PRODUCE launch the committed state (after this step's draw) is slot
+// cur, the host flips the slots, and cm.rng is brought up to date from it
+// (nv_commit_kernel) only before something reads it.  Streams are consumed in
+// the reference's order; arithmetic as nv_step_regs (newsvendor.py:125-204).
+template <int LT, bool HIT, bool PRODUCE>
+__global__ void __launch_bounds__(WAVE)
+nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
+    extern __shared__ __attribute__((aligned(16))) float nv_tile[];
+    const int lane = threadIdx.x;
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    const int O = P.L + 5;
+    double *lg_l = reinterpret_cast<double *>(nv_tile + ((EPW * O + 3) / 4) * 4);
+    const uint64_t *Acur = P.ahead + (int64_t)cur * 3 * S;
+    uint64_t *Anxt = P.ahead + (int64_t)(cur ^ 1) * 3 * S;
+    const int bid = (int)blockIdx.x;
+    if (HIT && bid < gla) {   // ---- lookahead workgroups
+        // PRODUCE: two workgroups per 64 envs, one per branch of numpy's sampler
+        // (bid even: PTRS for lam >= 10 and lam == 0; odd: the multiplication
+        // method for 0 < lam < 10), so a wave runs one branch, not both one
+        // after the other; a lane works only on the workgroup of its env's branch
+        const int64_t e = (int64_t)(PRODUCE ? bid >> 1 : bid) * WAVE + lane;
+        const bool valid = e < N;
+        const int64_t el = valid ? e : N - 1;
+        Pcg g;
+        g.hi = Acur[el];
+        g.lo = Acur[S + el];
+        if (PRODUCE) {
+            g.inc_hi = P.cm.rng.inc_hi[el];
+            g.inc_lo = P.cm.rng.inc_lo[el];
+            const double mu = P.par[4 * S + el];
+            const bool mult_wg = bid & 1;
+            TableStage ts;
+            if (!mult_wg) {
+                ts.dst = lg_l;
+                ts.load(P.lgtab, RHS_LDS_MAX, lane);
+                ts.flush(lane);
+            }
+            const bool mine = mult_wg == (mu < 10 && mu != 0);
+            if (mine) {
+                const int64_t dn = env_poisson_dyn(g, mu, lg_l, RHS_LDS_MAX);
+                if (valid) {
+                    st_store(Anxt + e, g.hi);
+                    st_store(Anxt + S + e, g.lo);
+                    st_store(Anxt + 2 * S + e, (uint64_t)dn);
+                }
+            }
+        } else if (valid) {
+            st_store(P.cm.rng.hi + e, g.hi);
+            st_store(P.cm.rng.lo + e, g.lo);
+        }
+        return;
+    }
+    const int64_t e0 = (int64_t)(bid - (HIT ? gla : 0)) * EPW;
+    const int64_t e = e0 + lane;
+    const bool valid = e < N;
+    const int nvalid = (int)((N - e0) < EPW ? (N - e0) : EPW);
+    const int64_t el = valid ? e : N - 1;
+    float *trow = nv_tile + (int64_t)lane * O;
+    constexpr int TILE_IT = (EPW * 21 * 4 + 16 * WAVE - 1) / (16 * WAVE);
+    NvState<LT> st;
+    TableStage ts;
+    int64_t dpre = -1;
+    if (HIT) {
+        dpre = (int64_t)Acur[2 * S + el];
+    } else {
+        st.g = P.cm.rng.load(el);
+        ts.dst = lg_l;
+        ts.load(P.lgtab, RHS_LDS_MAX, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < 5; j++) st.par[j] = P.par[j * S + el];
+    if (LT > 0) {
+        const int base = (int)((uint32_t)(sc + 1) % (uint32_t)(LT > 0 ? LT : 1));
+#pragma unroll
+        for (int p = 0; p < (LT > 0 ? LT : 1); p++) {
+            int sl = base + p;
+            sl = sl >= LT ? sl - LT : sl;
+            st.pv[p] = P.pipe[(int64_t)sl * S + el];
+            if (!(p >= LT - sc)) st.pv[p] = 0.f;
+        }
+    }
+    const float act = io.act[el];
+    double r;
+    const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, lg_l, HIT ? nullptr : &ts, r,
+                                     valid ? P.cm.info_demand : nullptr, dpre);
+    if (valid) {
+        out_store(io.rew + e, r);
+        out_store(io.term + e, (uint8_t)0);
+        out_store(io.trunc + e, (uint8_t)(tr ? 1 : 0));
+    }
+    wave_lds_sync();
+    store_tile<TILE_IT>(nv_tile, io.obs + e0 * O, (int64_t)nvalid * O, lane);
+    if (!HIT) {   // PRODUCE (the host runs nv_run_kernel for !HIT && !PRODUCE)
+        if (valid) {
+            st_store((uint64_t *)Acur + e, st.g.hi);
+            st_store((uint64_t *)Acur + S + e, st.g.lo);
+        }
+        const int64_t dn = env_poisson_dyn(st.g, st.par[4], lg_l, RHS_LDS_MAX);
+        if (valid) {
+            st_store(Anxt + e, st.g.hi);
+            st_store(Anxt + S + e, st.g.lo);
+            st_store(Anxt + 2 * S + e, (uint64_t)dn);
+        }
+    }
+}
+
+// cm.rng <- the committed slot of the lookahead cache
+__global__ void __launch_bounds__(256) nv_commit_kernel(NvParams P, int slot) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P.cm.N) return;
+    const int64_t S = P.cm.Npad;
+    const uint64_t *A = P.ahead + (int64_t)slot * 3 * S;
+    P.cm.rng.hi[e] = A[e];
+    P.cm.rng.lo[e] = A[S + e];
+}
+
+// INVSIM_NV_AHEAD=0 turns the demand lookahead off (A/B measurements)
+inline bool nv_ahead_enabled() {
+    const char *s = getenv("INVSIM_NV_AHEAD");
+    return !(s && s[0] == '0');
+}
+
 __global__ void __launch_bounds__(256)
 nv_reset_kernel(NvParams P, const uint8_t *__restrict__ mask, float *__restrict__ obs) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -310,13 +447,68 @@ inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / b
 
 }  // namespace
 
+hipError_t nv_commit_launch(const NvParams &p, int slot, hipStream_t s) {
+    if (p.cm.N == 0 || !p.ahead) return hipSuccess;
+    hipLaunchKernelGGL(nv_commit_kernel, dim3(grid_for(p.cm.N, 256)), dim3(256), 0, s, p, slot ^ 1);
+    return hipGetLastError();
+}
+
+#define NV_LT_SWITCH(L_)              \
+    switch (p.L) {                    \
+        case 0: L_(0); break;         \
+        case 1: L_(1); break;         \
+        case 2: L_(2); break;         \
+        case 3: L_(3); break;         \
+        case 4: L_(4); break;         \
+        case 5: L_(5); break;         \
+        case 6: L_(6); break;         \
+        case 7: L_(7); break;         \
+        case 8: L_(8); break;         \
+        case 9: L_(9); break;         \
+        case 10: L_(10); break;       \
+        case 12: L_(12); break;       \
+        case 16: L_(16); break;       \
+        default: L_(-1); break;       \
+    }
+
 hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
-                         hipStream_t s) {
+                         bool &ahead, int &slot, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = (size_t)((EPW * (p.L + 5) + 3) / 4) * 4 * sizeof(float) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
+    const bool la = p.ahead && nv_ahead_enabled();
+    if (la && !pol && io.K == 1 && t_u >= 0 && t_u < p.step_limit && io.obs &&
+        !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.step_limit)) {
+        const bool produce = t_u + 1 < p.step_limit;
+        if (ahead || produce) {
+            const bool hit = ahead;
+            const int gla = hit ? (produce ? 2 : 1) * (int)grid_for(p.cm.N, WAVE) : 0;
+            const dim3 grid2(grid.x + gla);
+            const int cur = slot;
+#define S_(X)                                                                                                \
+    do {                                                                                                     \
+        if (hit && produce) hipLaunchKernelGGL((nv_step1_kernel<X, true, true>), grid2, block, lds, s, p, t_u, io, cur, gla);  \
+        else if (hit) hipLaunchKernelGGL((nv_step1_kernel<X, true, false>), grid2, block, lds, s, p, t_u, io, cur, gla);       \
+        else hipLaunchKernelGGL((nv_step1_kernel<X, false, true>), grid2, block, lds, s, p, t_u, io, cur, gla);                \
+    } while (0)
+            NV_LT_SWITCH(S_)
+#undef S_
+            if (produce) {
+                ahead = true;
+                slot ^= 1;
+            } else {
+                ahead = false;   // cm.rng committed by the lookahead workgroups
+            }
+            return hipGetLastError();
+        }
+    }
+    if (ahead) {   // the one-wave kernel reads cm.rng: commit, the cache ends
+        const hipError_t ce = nv_commit_launch(p, slot, s);
+        ahead = false;
+        if (ce != hipSuccess) return ce;
+    }
 #define K_(X, TU, ONE, POL) \
     hipLaunchKernelGGL((nv_run_kernel<X, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
 #define L_(X)                                          \
@@ -332,22 +524,7 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
             else K_(X, false, false, false);           \
         }                                              \
     } while (0)
-    switch (p.L) {
-        case 0: L_(0); break;
-        case 1: L_(1); break;
-        case 2: L_(2); break;
-        case 3: L_(3); break;
-        case 4: L_(4); break;
-        case 5: L_(5); break;
-        case 6: L_(6); break;
-        case 7: L_(7); break;
-        case 8: L_(8); break;
-        case 9: L_(9); break;
-        case 10: L_(10); break;
-        case 12: L_(12); break;
-        case 16: L_(16); break;
-        default: L_(-1); break;
-    }
+    NV_LT_SWITCH(L_)
 #undef L_
 #undef K_
     return hipGetLastError();

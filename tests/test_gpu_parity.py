@@ -576,3 +576,76 @@ def test_invmgmt_demand_lookahead_mixed_calls(gpu, kw, monkeypatch):
     both(lambda env: env.reset())
     steps(12)
     same_state()
+
+
+@pytest.mark.parametrize("kw", [dict(autoreset_mode="next_step"), dict(autoreset_mode="disabled"),
+                                dict(autoreset_mode="same_step"), dict(autoreset_mode="next_step", mu_max=8.0)])
+def test_newsvendor_demand_lookahead_mixed_calls(gpu, kw, monkeypatch):
+    """Newsvendor's per-episode-rate demand lookahead (nv_step1_kernel): any
+    sequence of steps, rollouts, policy rollouts, seeds, resets (explicit,
+    masked, autoreset) and checkpoints gives the same outputs, demands and
+    state blobs as a run without the cache (INVSIM_NV_AHEAD=0).  Disabled
+    autoreset keeps stepping past step_limit (the reference does)."""
+    import invsim
+    from invsim.policies import OrderUpToHeuristicAgent
+    n = 700
+    envs = [invsim.NewsvendorEnv(n, device=gpu, step_limit=7, record_demand=True, **kw) for _ in range(2)]
+    g = torch.Generator(device=gpu).manual_seed(6)
+    A = torch.rand((100, n, 1), device=gpu, generator=g) * 400 - 20
+    pos = [0]
+
+    def both(fn):
+        outs = []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_NV_AHEAD", "1" if i == 0 else "0")
+            outs.append(fn(env))
+        return outs
+
+    def steps(k):
+        for _ in range(k):
+            a = A[pos[0] % 100]
+            pos[0] += 1
+
+            def one(env):
+                o, r, te, tr, info = env.step(a)
+                out = [o.clone(), r.clone(), te.clone(), tr.clone(), env._demand.clone()]
+                if "final_obs" in info:
+                    out.append(info["final_obs"][tr].clone())
+                return out
+            o = both(one)
+            for x, y in zip(o[0], o[1]):
+                assert torch.equal(x, y), pos[0]
+
+    def same_state():
+        s = both(lambda env: env.get_state().clone())
+        assert torch.equal(s[0], s[1]), pos[0]
+
+    both(lambda env: env.reset(seed=31))
+    steps(4)
+    same_state()
+    steps(5)                                                 # past step_limit
+    if kw["autoreset_mode"] == "disabled":
+        both(lambda env: env.reset())
+    o = both(lambda env: env.rollout(A[:3])) if kw["autoreset_mode"] != "same_step" else None
+    if o:
+        assert all(torch.equal(x, y) for x, y in zip(o[0], o[1]))
+    steps(2)
+    ck = both(lambda env: env.get_state().clone())
+    steps(3)
+    both(lambda env: env.reset(seed=32))
+    steps(2)
+    both(lambda env: env.set_state(ck[0].clone()))
+    steps(2)
+    both(lambda env: env.reset())
+    steps(3)
+    if kw["autoreset_mode"] != "same_step":
+        m = both(lambda env: env.rollout_policy(OrderUpToHeuristicAgent(), 2, obs=True))
+        assert all(torch.equal(m[0][k], m[1][k]) for k in m[0])
+    steps(2)
+    mask = torch.zeros(n, dtype=torch.bool, device=gpu)
+    mask[::4] = True
+    both(lambda env: env.reset(options={"reset_mask": mask}))
+    steps(2)
+    both(lambda env: env.reset())
+    steps(16)
+    same_state()
