@@ -12,7 +12,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"invmgmt_backlog": "im_split_kernel", "invmgmt_lostsales": "im_split_kernel",
-           "newsvendor": "nv_run_kernel", "net_backlog": "net_spec_kernel"}
+           "newsvendor": "nv_step1_kernel", "net_backlog": "net_spec_kernel"}
 
 
 def last_json(path):
