@@ -186,6 +186,12 @@ int invsim_status(invsim_handle *h, uint32_t *flags, int32_t clear);
  *   INVSIM_POLICY_BASE_STOCK   BaseStockAgent      benchmark_InvManagementBacklogEnv.py:142-198
  *                              (InvMgmt; also benchmark_InvManagementLostSalesEnv.py:137-165)
  *   INVSIM_POLICY_ORDER_UP_TO  OrderUpToHeuristicAgent  benchmark_newsvendor.py:97-111 (Newsvendor)
+ *   INVSIM_POLICY_CLASSIC_NV   ClassicNewsvendorAgent   benchmark_newsvendor.py:113-161 (Newsvendor;
+ *                              variant 0 = cr_method 'k_vs_h', 1 = 'profit_margin'; scipy
+ *                              poisson.ppf restated on device, newsvendor.hip nv_poisson_ppf)
+ *   INVSIM_POLICY_SS           sSPolicyAgent  benchmark_newsvendor_sb3_rllib.py:363-371 (Newsvendor;
+ *                              safety_factor carries S_buffer_factor)
+ * CLASSIC_NV / SS need mu_max * (lead_time + 1) * max(1, safety_factor) <= 1e6 (INVSIM_ERANGE).
  * Per-env metrics (f64, accumulated with += so a caller may chain launches),
  * the sums evaluate_agent keeps (benchmark_InvManagementBacklogEnv.py:346-440,
  * benchmark_NetInvMgmtLostSalesEnv.py:241-312, benchmark_newsvendor.py:219-250):
@@ -200,12 +206,14 @@ int invsim_status(invsim_handle *h, uint32_t *flags, int32_t clear);
 #define INVSIM_POLICY_CONSTANT 1
 #define INVSIM_POLICY_BASE_STOCK 2
 #define INVSIM_POLICY_ORDER_UP_TO 3
+#define INVSIM_POLICY_CLASSIC_NV 4
+#define INVSIM_POLICY_SS 5
 #define INVSIM_POLICY_MAX_ACTION 32
 
 typedef struct {
     int32_t kind;            /* INVSIM_POLICY_* */
-    int32_t reserved;
-    double safety_factor;    /* BASE_STOCK / ORDER_UP_TO */
+    int32_t variant;         /* CLASSIC_NV: 0 'k_vs_h', 1 'profit_margin'; else 0 */
+    double safety_factor;    /* BASE_STOCK / ORDER_UP_TO / CLASSIC_NV; SS: S_buffer_factor */
     double mu;               /* BASE_STOCK: env.dist_param.get('mu', 10) as the agent reads it */
     const void *constant;    /* CONSTANT: host array [action_dim] in the action dtype */
 } invsim_policy;

@@ -801,6 +801,7 @@ int invsim_rollout_policy(invsim_handle *h, int32_t K, const invsim_policy *poli
         return fail(h, INVSIM_EINVAL, "reward, terminated and truncated are given together or not at all");
     PolicyIO p{};
     p.kind = policy->kind;
+    p.variant = policy->variant;
     p.sf = policy->safety_factor;
     p.mu = policy->mu;
     p.act_out = actions;
@@ -821,6 +822,19 @@ int invsim_rollout_policy(invsim_handle *h, int32_t K, const invsim_policy *poli
         case INVSIM_POLICY_ORDER_UP_TO:
             if (h->family != INVSIM_NEWSVENDOR) return fail(h, INVSIM_EINVAL, "ORDER_UP_TO is a Newsvendor policy");
             break;
+        case INVSIM_POLICY_CLASSIC_NV:
+        case INVSIM_POLICY_SS: {
+            if (h->family != INVSIM_NEWSVENDOR)
+                return fail(h, INVSIM_EINVAL, "CLASSIC_NV / SS are Newsvendor policies");
+            if (policy->kind == INVSIM_POLICY_CLASSIC_NV && (policy->variant < 0 || policy->variant > 1))
+                return fail(h, INVSIM_EINVAL, "CLASSIC_NV variant: 0 'k_vs_h' or 1 'profit_margin'");
+            // the device ppf walks the Poisson CDF: bounded work per env
+            const double sf = policy->kind == INVSIM_POLICY_CLASSIC_NV ? policy->safety_factor : 1.0;
+            const double lam = (double)(float)h->nv.mu_max * (h->nv.L + 1) * (sf > 1 ? sf : 1.0);
+            if (!(lam <= 1e6))
+                return fail(h, INVSIM_ERANGE, "critical-ratio policies need mu_max * (lead_time + 1) * safety_factor <= 1e6");
+            break;
+        }
         default: return fail(h, INVSIM_EINVAL, "unknown policy kind");
     }
     DeviceGuard g(h->device);

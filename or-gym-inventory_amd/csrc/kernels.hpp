@@ -137,12 +137,15 @@ struct StepIO {
 // Closed-loop rollouts (invsim_rollout_policy): each step's action is computed
 // in the kernel from the env state by a restated heuristic agent, every output
 // is optional, and per-env evaluation metrics accumulate in registers.
-enum { POL_NONE = 0, POL_CONSTANT = 1, POL_BASE_STOCK = 2, POL_ORDER_UP_TO = 3 };
+enum { POL_NONE = 0, POL_CONSTANT = 1, POL_BASE_STOCK = 2, POL_ORDER_UP_TO = 3, POL_CLASSIC_NV = 4,
+       POL_SS = 5 };
 constexpr int POL_MAX_A = 32;
 struct PolicyIO {
     int32_t kind;
     int32_t mdim;             // metrics per env (0: none)
-    double sf, mu;            // safety factor; BASE_STOCK demand mean
+    int32_t variant;          // CLASSIC_NV: 0 'k_vs_h', 1 'profit_margin'
+    int32_t pad_;
+    double sf, mu;            // safety factor (SS: S_buffer_factor); BASE_STOCK demand mean
     int64_t ci[POL_MAX_A];    // CONSTANT actions, int64 action spaces
     float cf[POL_MAX_A];      // CONSTANT actions, f32 action spaces
     void *act_out;            // [K][N][action_dim] actions taken, may be null

@@ -120,6 +120,192 @@ __device__ __forceinline__ float nv_order_up_to(const NvParams &P, const PolicyI
     return (o > hi) ? hi : o;
 }
 
+// ---- scipy.stats.poisson.ppf for the critical-ratio agents --------------------
+// Third-party (scipy 1.15.3, not in the reference): rv_discrete.ppf gives -1 at
+// q == 0, inf at q == 1, NaN outside [0, 1]; otherwise poisson_gen._ppf:
+//     vals = ceil(pdtrik(q, mu)); vals1 = max(vals - 1, 0)
+//     return pdtr(vals1, mu) >= q ? vals1 : vals
+// The agents pass q and mu as np.float32, so scipy.special's float32 loops run:
+// pdtrik's root x* of the continuous CDF C(s) = Q(s + 1, mu) and pdtr are
+// rounded to float32.  Restated by exact arithmetic: j* = the smallest integer
+// with CDF(j) >= q; f32(x*) == j* - 1 exactly when x* < j* - 1 + ulp/2, i.e. when
+// C(j* - 1 + ulp/2) > q; then the pdtr test on the f32-rounded CDF.
+// (Residual: cdflib stops its root search at ~1e-11 relative, which decides
+// when x* lies that close to the rounding midpoint.)
+
+// R's dpois_raw (Loader's saddle point) for integer x > 35
+__device__ double ppf_dpois_raw(double x, double lam) {
+    const double nn = x * x;
+    const double S0 = 1.0 / 12, S1 = 1.0 / 360, S2 = 1.0 / 1260, S3 = 1.0 / 1680;
+    double st;
+    if (x > 500) st = (S0 - S1 / nn) / x;
+    else if (x > 80) st = (S0 - (S1 - S2 / nn) / nn) / x;
+    else st = (S0 - (S1 - (S2 - S3 / nn) / nn) / nn) / x;
+    const double d = x - lam;
+    double bd;
+    if (fabs(d) < 0.1 * (x + lam)) {
+        double v = d / (x + lam);
+        double s = d * v;
+        double ej = 2 * x * v;
+        v = v * v;
+        for (int j = 1; j < 1000; j++) {
+            ej *= v;
+            const double s1 = s + ej / (2 * j + 1);
+            if (s1 == s) break;
+            s = s1;
+        }
+        bd = s;
+    } else {
+        bd = x * log(x / lam) + lam - x;
+    }
+    return exp(-st - bd) / sqrt(2 * M_PI * x);
+}
+
+// regularised upper incomplete gamma Q(a, x), real a > 0, x > 0: series for
+// P below a + 1, modified Lentz continued fraction above
+__device__ double ppf_igamc(double a, double x) {
+    const double lpre = -x + a * log(x) - lgamma(a);
+    if (x < a + 1) {
+        double s = 1.0 / a, d = s;
+        for (int n = 1; n < 100000; n++) {
+            d *= x / (a + n);
+            s += d;
+            if (fabs(d) < fabs(s) * 1e-17) break;
+        }
+        return 1.0 - s * exp(lpre);
+    }
+    const double tiny = 1e-300;
+    double b = x + 1 - a, c = 1 / tiny, d = 1 / b, h = d;
+    for (int i = 1; i < 100000; i++) {
+        const double an = -i * (i - a);
+        b += 2;
+        d = an * d + b;
+        if (fabs(d) < tiny) d = tiny;
+        c = b + an / c;
+        if (fabs(c) < tiny) c = tiny;
+        d = 1 / d;
+        const double de = d * c;
+        h *= de;
+        if (fabs(de - 1) < 1e-16) break;
+    }
+    return exp(lpre) * h;
+}
+
+// poisson.ppf(q, mu); single: q and mu reach scipy as np.float32 (else float64)
+__device__ double nv_poisson_ppf(double q, double lam, bool single) {
+    if (q != q) return NAN;
+    if (q == 0) return -1.0;
+    if (q == 1) return INFINITY;
+    if (!(q > 0 && q < 1)) return NAN;
+    // bounded work per lane: the host refuses a policy whose mean can exceed 1e6;
+    // params injected past 1e7 by set_state give NaN (order 0)
+    if (!(lam <= 1e7)) return NAN;
+    // CDF by the pmf recurrence from i0, below which the mass is < 1e-80
+    const double sd = sqrt(lam);
+    double i0 = lam > 700 ? floor(lam - 20 * sd) : 0;
+    double p = (i0 > 0) ? ppf_dpois_raw(i0, lam) : exp(-lam);
+    double P = p, Pm1 = 0, Pm2 = 0;                                     // CDF(j), CDF(j-1), CDF(j-2)
+    double j = i0 > 0 ? i0 : 0;
+    const double jmax = lam + 40 * sd + 64;
+    while (P < q && j < jmax) {
+        j += 1;
+        p = p * lam / j;
+        Pm2 = Pm1;
+        Pm1 = P;
+        P += p;
+    }
+    if (!single) return j;                                              // float64 loops: exact j*
+    double vals = j;
+    if (j >= 2) {
+        int ex;
+        frexp(j - 1, &ex);                                              // j-1 in [2^(ex-1), 2^ex)
+        const double half = ldexp(1.0, ex - 1 - 24);                    // half an f32 ulp there
+        if (ppf_igamc(j + half, lam) > q) vals = j - 1;                 // f32(x*) == j - 1
+    }
+    const double vals1 = vals > 1 ? vals - 1 : 0;
+    const double c = (vals1 == j) ? P : (vals1 == j - 1) ? Pm1 : (vals1 == j - 2) ? Pm2 : 0.0;
+    return ((float)c >= (float)q) ? vals1 : vals;
+}
+
+// ClassicNewsvendorAgent.get_action (benchmark_newsvendor.py:121-161).  The
+// observation's params are float32 and every expression keeps numpy's dtypes:
+// the critical ratio and the effective mean are float32, poisson.ppf returns
+// float64, and the order is clipped in float64 and cast to float32.  The ppf
+// level depends only on the episode's params: computed once per episode (lvl).
+template <int LT>
+__device__ __forceinline__ float nv_classic(const NvParams &P, const PolicyIO &pol, int64_t e, int sc,
+                                            const NvState<LT> &s, double &lvl, bool &have) {
+    const int L = (LT >= 0) ? LT : P.L;
+    const float price = (float)s.par[0], cost = (float)s.par[1], h = (float)s.par[2], k = (float)s.par[3],
+                mu = (float)s.par[4];
+    const float eps = 1e-6f;                                            // Python 1e-6 against float32 (NEP 50)
+    bool fb;
+    float cr = 0.f;
+    if (pol.variant == 1) {                                             // 'profit_margin' (:128-134)
+        const float under = (price - cost) + k, over = h;
+        fb = (under + over <= eps) || (under <= 0.f) || (over <= 0.f);
+        if (!fb) cr = under / (under + over);
+    } else {                                                            // 'k_vs_h' and default (:135-142)
+        fb = (h + k <= eps) || (k < 0.f) || (h < 0.f);
+        if (!fb) cr = k / (h + k);
+    }
+    const float pos = nv_pipe_sum<LT>(P, e, sc, s);                     // pipeline_inventory.sum()
+    const float hi = (float)P.max_order;
+    if (fb) {                                                           // :144-148, float32
+        const float q = mu * (float)(L + 1) - pos;
+        float o = (q > 0.f) ? q : 0.f;
+        o = (o < 0.f) ? 0.f : o;
+        return (o > hi) ? hi : o;
+    }
+    if (!have) {                                                        // :151-153
+        const float eff = (mu * (float)(L + 1)) * (float)pol.sf;
+        const bool f = eff > eps;                                       // max(1e-6, effective_mu)
+        lvl = nv_poisson_ppf((double)cr, f ? (double)eff : 1e-6, f);
+        have = true;
+    }
+    const double d = lvl - (double)pos;                                 // float64 - float32
+    double o = (d > 0) ? d : 0.0;                                       // builtin max(0, .)
+    o = (o < 0.0) ? 0.0 : o;                                            // np.clip (:160)
+    o = (o > (double)hi) ? (double)hi : o;
+    return (float)o;
+}
+
+// sSPolicyAgent.get_action (benchmark_newsvendor_sb3_rllib.py:363-371, the
+// module's last definition): s = ppf(clip(k / (h + k), 0.001, 0.999), mu (L + 1))
+// in float32 inputs, S = s * S_buffer_factor; order up to S when the pipeline is
+// below s.  The level s is per episode (lvl).
+template <int LT>
+__device__ __forceinline__ float nv_ss(const NvParams &P, const PolicyIO &pol, int64_t e, int sc,
+                                       const NvState<LT> &s, double &lvl, bool &have) {
+    const int L = (LT >= 0) ? LT : P.L;
+    if (!have) {
+        const float h = (float)s.par[2], k = (float)s.par[3], mu = (float)s.par[4];
+        const float eps = 1e-6f;
+        double sl = 0.0;                                                // s_lvl = 0
+        if (h + k > eps) {
+            float q = k / (h + k);
+            q = (q < 0.001f) ? 0.001f : q;                              // np.clip(cr_s, 0.001, 0.999): float32
+            q = (q > 0.999f) ? 0.999f : q;
+            const float eff = mu * (float)(L + 1);
+            const bool f = eff > eps;
+            sl = nv_poisson_ppf((double)q, f ? (double)eff : 1e-6, f);
+        }
+        lvl = (sl > 0) ? sl : 0.0;                                      // s_level = max(0, s_lvl)
+        have = true;
+    }
+    const float pos = nv_pipe_sum<LT>(P, e, sc, s);
+    const double S_level = lvl * pol.sf;
+    double o = 0.0;
+    if ((double)pos < lvl) {
+        const double d = S_level - (double)pos;
+        o = (d > 0) ? d : 0.0;
+    }
+    const double hi = (double)(float)P.max_order;
+    o = (o < 0.0) ? 0.0 : o;
+    o = (o > hi) ? hi : o;
+    return (float)o;
+}
+
 // One newsvendor.py:125-204 step at step count sc.  Returns truncated.
 template <int LT>
 __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool valid, int sc, NvState<LT> &s,
@@ -236,6 +422,8 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
 #pragma unroll
     for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
     const int K = ONE ? 1 : io.K;
+    double lvl = 0.0;     // CLASSIC_NV / SS: the episode's ppf level, once computed
+    bool have = false;
     // all lanes write the table: before any divergent step/reset branch (with a
     // lock-step single step there is none, and the write waits inside the step)
     if (!(ONE && TU)) ts.flush(lane);
@@ -245,6 +433,7 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
         if (!POL) act = io.act[(int64_t)k * N + el];
         if (!(ONE && TU) && P.cm.autoreset == AR_NEXT_STEP && sc >= P.step_limit) {
             nv_reset_regs<LT>(P, e, st, trow, valid);
+            have = false;
             if (valid && (!POL || io.rew)) {
                 out_store(io.rew + oi, 0.0);
                 out_store(io.term + oi, (uint8_t)0);
@@ -254,7 +443,10 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
         } else {
             double r;
             if (POL) {
-                act = (pol.kind == POL_ORDER_UP_TO) ? nv_order_up_to<LT>(P, pol, e, sc, st) : pol.cf[0];
+                if (pol.kind == POL_ORDER_UP_TO) act = nv_order_up_to<LT>(P, pol, e, sc, st);
+                else if (pol.kind == POL_CLASSIC_NV) act = nv_classic<LT>(P, pol, e, sc, st, lvl, have);
+                else if (pol.kind == POL_SS) act = nv_ss<LT>(P, pol, e, sc, st, lvl, have);
+                else act = pol.cf[0];
                 if (valid && pol.act_out) out_store((float *)pol.act_out + oi, act);
             }
             const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, ts.dst, (ONE && TU) ? &ts : nullptr, r,
@@ -275,6 +467,7 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
                     for (int j = 0; j < O; j++) io.fobs[e * O + j] = trow[j];
                 wave_lds_sync();
                 nv_reset_regs<LT>(P, e, st, trow, valid);
+                have = false;
                 sc = 0;
             }
         }

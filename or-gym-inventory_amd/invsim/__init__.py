@@ -24,6 +24,8 @@ _LAZY = {
     "BaseStockAgent": "policies",
     "ConstantOrderAgent": "policies",
     "OrderUpToHeuristicAgent": "policies",
+    "ClassicNewsvendorAgent": "policies",
+    "sSPolicyAgent": "policies",
     "evaluate_agent": "policies",
     "rollout_policy": "policies",
 }

@@ -56,11 +56,11 @@ class NetInvMgmtSpec(C.Structure):
         (n, C.c_void_p) for n in NET_TABLE_FIELDS]
 
 
-POLICY_KINDS = {"constant": 1, "base_stock": 2, "order_up_to": 3}
+POLICY_KINDS = {"constant": 1, "base_stock": 2, "order_up_to": 3, "classic_nv": 4, "ss": 5}
 
 
 class PolicySpec(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32), ("safety_factor", C.c_double),
+    _fields_ = [("kind", C.c_int32), ("variant", C.c_int32), ("safety_factor", C.c_double),
                 ("mu", C.c_double), ("constant", C.c_void_p)]
 
 

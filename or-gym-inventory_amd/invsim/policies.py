@@ -13,6 +13,10 @@ Agents (restated from the reference, same names and constructor arguments):
 * ``ConstantOrderAgent(order_fraction)``   benchmark_NetInvMgmtBacklogEnv.py:119-135
   (and benchmark_NetInvMgmtLostSalesEnv.py:131-142), any env
 * ``OrderUpToHeuristicAgent(safety_factor)`` benchmark_newsvendor.py:97-111, Newsvendor
+* ``ClassicNewsvendorAgent(cr_method, safety_factor)`` benchmark_newsvendor.py:113-161,
+  Newsvendor (scipy ``poisson.ppf`` restated on device, float32 loops included)
+* ``sSPolicyAgent(s_quantile, S_buffer_factor)`` benchmark_newsvendor_sb3_rllib.py:363-371,
+  Newsvendor (the module's last definition; ``s_quantile`` is unused there too)
 
 ``evaluate_agent(agent, env_cls, env_config, n_episodes, seed_offset)`` returns
 the reference's summary columns (benchmark_InvManagementBacklogEnv.py:346-440,
@@ -80,6 +84,40 @@ class OrderUpToHeuristicAgent(_Agent):
         if env.family != _capi.INVSIM_NEWSVENDOR:
             raise TypeError("OrderUpToHeuristicAgent needs a Newsvendor env")
         return _capi.PolicySpec(_capi.POLICY_KINDS["order_up_to"], 0, float(self.safety_factor), 0.0, None), None
+
+
+class ClassicNewsvendorAgent(_Agent):
+    """Order up to poisson.ppf(critical ratio, mu * (lead_time + 1) * sf) over
+    the pipeline; cr_method 'k_vs_h' (k / (h + k), also any unknown method) or
+    'profit_margin' ((p - c + k) / (p - c + k + h)), falling back to OrderUpTo
+    without the safety factor when the ratio is undefined."""
+
+    def __init__(self, cr_method="k_vs_h", safety_factor=1.0):
+        self.name = f"ClassicNV_SF={safety_factor:.1f}_{cr_method}"
+        self.cr_method = cr_method
+        self.safety_factor = safety_factor
+
+    def device_spec(self, env):
+        if env.family != _capi.INVSIM_NEWSVENDOR:
+            raise TypeError("ClassicNewsvendorAgent needs a Newsvendor env")
+        variant = 1 if self.cr_method == "profit_margin" else 0
+        return _capi.PolicySpec(_capi.POLICY_KINDS["classic_nv"], variant, float(self.safety_factor), 0.0,
+                                None), None
+
+
+class sSPolicyAgent(_Agent):
+    """(s, S): s = poisson.ppf(clip(k / (h + k), 0.001, 0.999), mu * (lead_time + 1)),
+    S = s * S_buffer_factor; order S - position when the position is below s."""
+
+    def __init__(self, s_quantile=0.5, S_buffer_factor=1.2):
+        self.name = f"sS_Policy(s={s_quantile:.2f},S={S_buffer_factor:.1f}s)"
+        self.s_quantile = s_quantile
+        self.S_buffer_factor = S_buffer_factor
+
+    def device_spec(self, env):
+        if env.family != _capi.INVSIM_NEWSVENDOR:
+            raise TypeError("sSPolicyAgent needs a Newsvendor env")
+        return _capi.PolicySpec(_capi.POLICY_KINDS["ss"], 0, float(self.S_buffer_factor), 0.0, None), None
 
 
 def rollout_policy(env, agent, K, obs=False, rewards=True, actions=False, metrics=None):

@@ -7,6 +7,9 @@ uses there:
 
 * base_stock       BaseStockAgent.get_action  benchmark_InvManagementBacklogEnv.py:152-198
 * order_up_to      OrderUpToHeuristicAgent    benchmark_newsvendor.py:103-111
+* classic_nv       ClassicNewsvendorAgent     benchmark_newsvendor.py:121-161 (calls the
+                   third-party scipy.stats.poisson.ppf itself, as the reference does)
+* ss_policy        sSPolicyAgent              benchmark_newsvendor_sb3_rllib.py:363-371
 * constant_order   ConstantOrderAgent         benchmark_NetInvMgmtBacklogEnv.py:127-135
 * run_*            evaluate_agent's per-episode sums
                    benchmark_InvManagementBacklogEnv.py:364-399,
@@ -50,6 +53,58 @@ def order_up_to(obs, lead_time, sf, max_order):
     return out
 
 
+def classic_nv(obs, lead_time, sf, max_order, cr_method="k_vs_h"):
+    """obs [N, 5 + L] float32 -> action [N, 1] float32, per-env numpy scalars."""
+    from scipy.stats import poisson
+    out = np.zeros((obs.shape[0], 1), np.float32)
+    for n in range(obs.shape[0]):
+        price, cost, h, k, mu = obs[n, :5]
+        pipeline = obs[n, 5:]
+        fallback = False
+        if cr_method == "profit_margin":
+            under = price - cost + k
+            over = h
+            if under + over <= 1e-6 or under <= 0 or over <= 0:
+                fallback = True
+            else:
+                cr = under / (under + over)
+        else:
+            if h + k <= 1e-6 or k < 0 or h < 0:
+                fallback = True
+            else:
+                cr = k / (h + k)
+        if fallback:
+            target = mu * (lead_time + 1)
+            q = max(0, target - pipeline.sum())
+        else:
+            eff = mu * (lead_time + 1) * sf
+            level = poisson.ppf(cr, mu=max(1e-6, eff))
+            q = max(0, level - pipeline.sum())
+        out[n, 0] = np.array([np.clip(q, np.float32(0), np.float32(max_order))], dtype=np.float32)[0]
+    return out
+
+
+def ss_policy(obs, lead_time, S_buffer_factor, max_order):
+    from scipy.stats import poisson
+    out = np.zeros((obs.shape[0], 1), np.float32)
+    for n in range(obs.shape[0]):
+        price, cost, h, k, mu = obs[n, :5]
+        pipe = obs[n, 5:]
+        s_lvl = 0
+        if h + k > 1e-6:
+            cr_s = k / (h + k)
+            eff = mu * (lead_time + 1)
+            s_lvl = poisson.ppf(np.clip(cr_s, 0.001, 0.999), mu=max(1e-6, eff))
+        s_level = max(0, s_lvl)
+        S_level = s_level * S_buffer_factor
+        pos = pipe.sum()
+        order = 0
+        if pos < s_level:
+            order = max(0, S_level - pos)
+        out[n, 0] = np.array([np.clip(order, np.float32(0), np.float32(max_order))], dtype=np.float32)[0]
+    return out
+
+
 def constant_order(high, fraction, dtype):
     high = np.array(high, copy=True)
     high[high == np.inf] = 1000
@@ -78,12 +133,17 @@ def run_invmgmt(orc, obs, steps, L, mu, sf, c, period0=0):
     return np.stack(acts), np.stack(rews), np.stack(obss), sums
 
 
-def run_newsvendor(orc, obs, steps, lead_time, sf, max_order):
+def run_newsvendor(orc, obs, steps, lead_time, sf, max_order, agent="order_up_to", cr_method="k_vs_h"):
     N = obs.shape[0]
     sums = np.zeros((N, 2))
     acts, rews, obss = [], [], []
     for _ in range(steps):
-        a = order_up_to(obs, lead_time, sf, max_order)
+        if agent == "classic_nv":
+            a = classic_nv(obs, lead_time, sf, max_order, cr_method)
+        elif agent == "ss":
+            a = ss_policy(obs, lead_time, sf, max_order)
+        else:
+            a = order_up_to(obs, lead_time, sf, max_order)
         obs, r, tr, _ = orc.step(a)
         sums[:, 0] += r
         sums[:, 1] += 1

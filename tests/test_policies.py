@@ -147,3 +147,190 @@ def test_evaluate_agent_columns(gpu, oracle):
     assert np.array_equal(res["AvgServiceLevel"], np.array(sl))
     assert np.array_equal(res["AvgEndingInv"], s[:, 5] / 30)
     assert res["Seed"].tolist() == list(range(1000, 1200)) and res["Agent"][0] == "BaseStock_SF=1.0"
+
+
+# ---- ClassicNewsvendorAgent / sSPolicyAgent: scipy.stats.poisson.ppf on device ----
+# The third-party scipy (1.15.3 here and on the GPU box) is the pin: the agents'
+# oracle calls poisson.ppf itself, as the reference does.  tests/ppf_model.py
+# is the device algorithm in Python.
+
+def _ppf_boundary_cases(rng, n_mu):
+    """(q, mu) float32 pairs where scipy's float32 loops decide: q a few ulps
+    around CDF(j), and q putting pdtrik's root x* just below / above the f32
+    rounding midpoint above an integer."""
+    from scipy import special
+    f32 = np.float32
+    out = []
+    for _ in range(n_mu):
+        mu = f32(rng.random() * 1200 + 0.5)
+        j = int(max(0, round(float(mu) + rng.normal() * np.sqrt(float(mu)) * 2)))
+        q0 = f32(special.pdtr(j, float(mu)))
+        for d in range(-3, 4):
+            q = q0
+            for _ in range(abs(d)):
+                q = np.nextafter(q, f32(1) if d > 0 else f32(0))
+            out.append((q, mu))
+        if j >= 1:
+            half = 2.0 ** (np.floor(np.log2(j)) - 24)
+            for t in (0.5, 0.9, 1.1, 1.5):
+                out.append((f32(special.gammaincc(j + 1 + half * t, float(mu))), mu))
+    return [(q, mu) for q, mu in out if 0 < q < 1]
+
+
+def test_ppf_model_vs_scipy_random():
+    from scipy.stats import poisson
+    import ppf_model
+    f32 = np.float32
+    rng = np.random.default_rng(5)
+    for it in range(3000):
+        h, k, mu = f32(rng.random() * 5), f32(rng.random() * 10), f32(rng.random() * 200)
+        L, sf = [0, 1, 5, 9][it % 4], [1.0, 1.2, 0.8, 2.0][(it // 4) % 4]
+        q = k / (h + k)
+        eff = mu * (L + 1) * sf
+        m = max(1e-6, eff)
+        exp = float(poisson.ppf(q, mu=m))
+        assert ppf_model.ppf(float(q), float(m), isinstance(m, np.float32)) == exp, (q, m)
+
+
+def test_ppf_model_vs_scipy_float32_boundaries():
+    """Near the boundaries scipy's float32 loops decide the answer: the model
+    matches scipy where a float64 inverse does not."""
+    from scipy.stats import poisson
+    import ppf_model
+    cases = _ppf_boundary_cases(np.random.default_rng(11), 400)
+    assert len(cases) > 3000
+    plain_wrong = 0
+    for q, mu in cases:
+        exp = float(poisson.ppf(q, mu=mu))
+        assert ppf_model.ppf(float(q), float(mu), True) == exp, (float(q), float(mu))
+        plain_wrong += ppf_model.ppf(float(q), float(mu), False) != exp
+    assert plain_wrong > len(cases) // 10
+
+
+def test_classic_nv_restatement_hand_cases():
+    from scipy.stats import poisson
+    f32 = np.float32
+    obs = np.zeros((4, 7), np.float32)
+    obs[:, :5] = [[50, 20, 2, 6, 30], [50, 20, 0, 0, 30], [10, 20, 1, 3, 12.5], [50, 20, 2, 6, 30]]
+    obs[3, 5:] = [400, 500]
+    a = agents.classic_nv(obs, 2, 1.0, 2000)
+    assert a.dtype == np.float32
+    assert a[0, 0] == poisson.ppf(f32(6) / f32(8), mu=f32(90))              # k / (h + k)
+    assert a[1, 0] == f32(30) * 3                                           # h + k = 0: fallback
+    assert a[3, 0] == 0.0                                                   # position above the level
+    b = agents.classic_nv(obs, 2, 1.0, 2000, "profit_margin")
+    assert b[2, 0] == f32(12.5) * 3                                         # p - c + k <= 0: fallback
+    u = f32(50) - f32(20) + f32(6)
+    assert b[0, 0] == poisson.ppf(u / (u + f32(2)), mu=f32(90))
+    s = agents.ss_policy(obs, 2, 1.2, 2000)
+    lvl = poisson.ppf(f32(0.75), mu=f32(90))
+    assert s[0, 0] == f32(lvl * 1.2) and s[1, 0] == 0.0 and s[3, 0] == 0.0
+
+
+def _nv_pair(gpu, oracle, n, L, seed):
+    import invsim
+    env = invsim.NewsvendorEnv(n, device=gpu, lead_time=L, autoreset_mode="disabled")
+    orc = oracle.OracleNewsvendor(n, lead_time=L)
+    orc.seed(range(seed, seed + n))
+    o0 = orc.reset()
+    env.reset(seed=seed)
+    return env, orc, o0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cr,sf,L", [("k_vs_h", 1.0, 5), ("k_vs_h", 1.3, 2), ("profit_margin", 1.0, 5),
+                                     ("profit_margin", 0.7, 0), ("other", 1.0, 9)])
+def test_classic_nv_vs_oracle(gpu, oracle, cr, sf, L):
+    import torch
+    import invsim
+    n = 500
+    env, orc, o0 = _nv_pair(gpu, oracle, n, L, 2000)
+    met = torch.zeros((n, 2), dtype=torch.float64, device=gpu)
+    out = env.rollout_policy(invsim.ClassicNewsvendorAgent(cr, sf), 40, obs=True, actions=True, metrics=met)
+    e_act, e_rew, e_obs, e_sum = agents.run_newsvendor(orc, o0, 40, L, sf, 2000, "classic_nv", cr)
+    assert np.array_equal(out["actions"].cpu().numpy().view(np.uint32), e_act.view(np.uint32))
+    assert np.array_equal(out["obs"].cpu().numpy().view(np.uint32), e_obs.view(np.uint32))
+    assert np.array_equal(out["reward"].cpu().numpy().view(np.uint64), e_rew.view(np.uint64))
+    assert np.array_equal(met.cpu().numpy().view(np.uint64), e_sum.view(np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sbf,L", [(1.2, 5), (1.0, 0), (2.5, 3)])
+def test_ss_policy_vs_oracle(gpu, oracle, sbf, L):
+    import torch
+    import invsim
+    n = 500
+    env, orc, o0 = _nv_pair(gpu, oracle, n, L, 3000)
+    met = torch.zeros((n, 2), dtype=torch.float64, device=gpu)
+    out = env.rollout_policy(invsim.sSPolicyAgent(0.5, sbf), 40, obs=True, actions=True, metrics=met)
+    e_act, e_rew, e_obs, e_sum = agents.run_newsvendor(orc, o0, 40, L, sbf, 2000, "ss")
+    assert np.array_equal(out["actions"].cpu().numpy().view(np.uint32), e_act.view(np.uint32))
+    assert np.array_equal(out["reward"].cpu().numpy().view(np.uint64), e_rew.view(np.uint64))
+    assert np.array_equal(met.cpu().numpy().view(np.uint64), e_sum.view(np.uint64))
+
+
+@pytest.mark.gpu
+def test_classic_nv_ppf_boundaries_on_device(gpu):
+    """Episode params injected (set_state) so that k / (h + k) and mu sit on
+    the float32 decision boundaries of scipy's ppf; the first action is the
+    ppf level itself (empty pipeline, L = 0)."""
+    import invsim
+    import ppf_model
+    f32 = np.float32
+    pairs = []
+    for q, mu in _ppf_boundary_cases(np.random.default_rng(23), 250):
+        k = f32(float(q) / (1.0 - float(q)))
+        for _ in range(8):                                  # f32 k with f32(k / (1 + k)) == q
+            r = k / (f32(1) + k)
+            if r == q:
+                pairs.append((k, mu))
+                break
+            k = np.nextafter(k, f32(np.inf) if r < q else f32(0))
+    assert len(pairs) > 1000
+    n = len(pairs)
+    env = invsim.NewsvendorEnv(n, device=gpu, lead_time=0, autoreset_mode="disabled")
+    env.reset(seed=1)
+    blob = env.get_state()
+    par = env.state_fields(blob)["params"]                  # [5, N] f64 bits
+    p = np.zeros((5, n))
+    p[0], p[1], p[2] = 50.0, 20.0, 1.0
+    p[3] = [float(k) for k, _ in pairs]
+    p[4] = [float(mu) for _, mu in pairs]
+    par.copy_(torch_from(p, par))
+    env.set_state(blob)
+    out = env.rollout_policy(invsim.ClassicNewsvendorAgent(), 1, rewards=False, actions=True)
+    got = out["actions"][0, :, 0].cpu().numpy()
+    obs = np.zeros((n, 5), np.float32)
+    obs[:] = p.T
+    exp = agents.classic_nv(obs, 0, 1.0, 2000)[:, 0]
+    model = np.array([ppf_model.ppf(float(k / (f32(1) + k)), float(mu), True) for k, mu in pairs], np.float32)
+    assert np.array_equal(got, model)
+    assert np.array_equal(got, exp)
+
+
+def torch_from(a, like):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).view(torch.int64).to(like.device)
+
+
+@pytest.mark.gpu
+def test_classic_nv_across_autoresets(gpu, oracle):
+    """NEXT_STEP autoreset inside one policy launch: the per-episode ppf level
+    is recomputed for the new episode's params."""
+    import invsim
+    n, L = 300, 5
+    env = invsim.NewsvendorEnv(n, device=gpu, lead_time=L, step_limit=12)
+    orc = oracle.OracleNewsvendor(n, lead_time=L, step_limit=12)
+    orc.seed(range(70, 70 + n))
+    o0 = orc.reset()
+    env.reset(seed=70)
+    out = env.rollout_policy(invsim.ClassicNewsvendorAgent("k_vs_h", 1.1), 25, obs=True, actions=True)
+    a1, r1, ob1, _ = agents.run_newsvendor(orc, o0, 12, L, 1.1, 2000, "classic_nv")
+    o1 = orc.reset()
+    a2, r2, ob2, _ = agents.run_newsvendor(orc, o1, 12, L, 1.1, 2000, "classic_nv")
+    acts = out["actions"].cpu().numpy()
+    assert np.array_equal(acts[:12], a1) and np.array_equal(acts[13:], a2)
+    obs = out["obs"].cpu().numpy()
+    assert np.array_equal(obs[12], o1) and np.array_equal(obs[13:], ob2)
+    rew = out["reward"].cpu().numpy()
+    assert np.array_equal(rew[:12], r1) and np.array_equal(rew[13:], r2) and not rew[12].any()
