@@ -649,3 +649,41 @@ def test_newsvendor_demand_lookahead_mixed_calls(gpu, kw, monkeypatch):
     both(lambda env: env.reset())
     steps(16)
     same_state()
+
+
+@pytest.mark.parametrize("cls,n,pre,Ks,mode", [
+    ("InvManagementBacklogEnv", 4000, 0, (75, 2, 9), "next_step"),
+    ("InvManagementLostSalesEnv", 4000, 7, (40, 16, 3), "next_step"),
+    ("InvManagementBacklogEnv", 65536, 3, (61,), "next_step"),
+    ("InvManagementBacklogEnv", 1000, 5, (8, 17), "disabled"),
+])
+def test_invmgmt_register_window_rollout_equals_one_wave(gpu, monkeypatch, cls, n, pre, Ks, mode):
+    """invsim_rollout of the default lead times runs im_roll3_kernel (register
+    windows + demand wave); INVSIM_IM_ROLL=0 keeps it on the one-wave kernel.
+    Both paths from the same state: identical outputs, demand record and state
+    (wide >= 2^32 orders included)."""
+    import invsim
+    envs = []
+    for i in range(2):
+        env = getattr(invsim, cls)(n, device=gpu, autoreset_mode=mode, record_demand=True)
+        env.reset(seed=41)
+        envs.append(env)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(9)
+    for k in range(pre):
+        a = torch.randint(0, 260, (n, 3), device=gpu, dtype=torch.int64, generator=g)
+        for env in envs:
+            env.step(a)
+    for K in Ks:
+        a = torch.randint(-5, 260, (K, n, 3), device=gpu, dtype=torch.int64, generator=g)
+        a[:, ::97, 1] = (1 << 32) + 5          # wide requested orders: the int64 side ring
+        outs, dems = [], []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_IM_ROLL", "1" if i == 0 else "0")
+            outs.append(env.rollout(a))
+            dems.append(env._demand.clone())
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), K
+        assert torch.equal(dems[0], dems[1])
+        assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
+    monkeypatch.delenv("INVSIM_IM_ROLL")
