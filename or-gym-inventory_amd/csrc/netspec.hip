@@ -56,21 +56,25 @@ __device__ __forceinline__ void spec_reset(NetSt<G> &s, float *orow) {
     for (int q = 0; q < G::sumL; q++) orow[G::RL + G::J + q] = 0.f;
 }
 
-// One step (:436-635) at period t < T; obs row into orow (LDS).  Returns the
-// reward; Rn receives R[t] (the fulfilled orders) per link.
+// market demand draws of one step, retail-link order: max(0, int(round(poisson(lam))))
+// (:536-541)
 template <class G>
-__device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst (&pc)[G::RL], const double *rhs_l,
-                                            int t, double apow, NetSt<G> &s, const float (&act)[G::E],
-                                            float *orow, double (&Rn)[G::E], int64_t (&dem)[G::RL],
-                                            double *met, double *irec) {
-    // market demand draws, retail-link order (:536-541)
-    double Dd[G::RL];
+__device__ __forceinline__ void spec_demand(Pcg &g, const PtrsConst (&pc)[G::RL], const double *rhs_l,
+                                            double (&Dd)[G::RL]) {
 #pragma unroll
     for (int r = 0; r < G::RL; r++) {
-        const int64_t pd = np_poisson(s.g, pc[r], rhs_l + r * RHS_LDS_MAX);
+        const int64_t pd = np_poisson(g, pc[r], rhs_l + r * RHS_LDS_MAX);
         Dd[r] = (double)(pd > 0 ? pd : 0);
-        dem[r] = (int64_t)Dd[r];
     }
+}
+
+// One step (:436-635) at period t < T given the step's market demands Dd; obs
+// row into orow (LDS).  Returns the reward; Rn receives R[t] (the fulfilled
+// orders) per link.
+template <class G>
+__device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apow, NetSt<G> &s,
+                                           const float (&act)[G::E], const double (&Dd)[G::RL], float *orow,
+                                           double (&Rn)[G::E], double *met, double *irec) {
     double cons[G::J];
 #pragma unroll
     for (int j = 0; j < G::J; j++) cons[j] = 0.0;
@@ -196,6 +200,19 @@ __device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst 
     }
     (void)t;
     return apow * total;                                       // :619
+}
+
+// One step (:436-635) at period t < T: the demand draws, then the dynamics
+template <class G>
+__device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst (&pc)[G::RL], const double *rhs_l,
+                                            int t, double apow, NetSt<G> &s, const float (&act)[G::E],
+                                            float *orow, double (&Rn)[G::E], int64_t (&dem)[G::RL],
+                                            double *met, double *irec) {
+    double Dd[G::RL];
+    spec_demand<G>(s.g, pc, rhs_l, Dd);
+#pragma unroll
+    for (int r = 0; r < G::RL; r++) dem[r] = (int64_t)Dd[r];
+    return spec_dyn<G>(P, t, apow, s, act, Dd, orow, Rn, met, irec);
 }
 
 // shift the age-aligned windows by one period: age a+1 <- age a, age 1 <- R[t]
@@ -408,6 +425,197 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     (void)t_start;
 }
 
+// Cross-wave LDS handoff inside a workgroup: orders LDS traffic only (an
+// __syncthreads() would also drain each wave's outstanding global loads and
+// stores, s_waitcnt vmcnt(0), before the s_barrier)
+__device__ __forceinline__ void net_wg_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// K-step lock-step rollout (invsim_rollout without a policy, NEXT_STEP
+// autoreset or no overrun, Poisson market demand) of a compiled network, one
+// 128-thread workgroup per 64 envs:
+//   wave 0 (demand)   draws the market demands (RL per step, retail-link order)
+//                     of CH launch steps at a time into a double-buffered LDS
+//                     ring, ahead of the dynamics wave.  A demand is a function
+//                     of the env's stream only (the orders never touch it), and
+//                     a NEXT_STEP reset step draws nothing (reset(), :301-332).
+//   wave 1 (dynamics) spec_dyn with the windows in registers; a step's actions
+//                     and alpha**t are loaded one step ahead, before the
+//                     previous step's stores (vmcnt is in order: a load issued
+//                     behind stores waits for them).
+// Chunk handoff: the demand wave fills buffer c & 1, then barrier c; the
+// dynamics wave consumes chunk c after barrier c, so a buffer's refill follows
+// its use.  Same arithmetic, in the same order, as net_spec_kernel.
+template <class G>
+struct NetRoll {
+    static constexpr int CH = 8;                                          // demand chunk (launch steps)
+    static constexpr size_t tile_bytes() { return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float); }
+    static constexpr size_t lds() {
+        return tile_bytes() + (size_t)G::RL * RHS_LDS_MAX * sizeof(double) + 2 * (size_t)CH * G::RL * WAVE * sizeof(double);
+    }
+};
+
+template <class G>
+__global__ void __launch_bounds__(2 * WAVE)
+net_roll_kernel(NetParams P, int t_start, StepIO<float, float> io) {
+    using R = NetRoll<G>;
+    constexpr int O = G::O, CH = R::CH, RL = G::RL;
+    constexpr int TILE_IT = (EPW * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
+    extern __shared__ __attribute__((aligned(16))) float nr_lds[];
+    float *tile = nr_lds;
+    double *rhs_l = reinterpret_cast<double *>(nr_lds + R::tile_bytes() / sizeof(float));
+    double *dbuf = rhs_l + RL * RHS_LDS_MAX;                          // [2][CH][RL][WAVE]
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e = e0 + lane;
+    const bool valid = e < N;
+    const int64_t el = valid ? e : N - 1;       // padded lanes: the last env's data, never stored
+    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
+    const int K = io.K;
+    const int nch = (K + CH - 1) / CH;
+    if (threadIdx.x < WAVE) {   // ---- demand wave
+        PtrsConst pc[RL];
+#pragma unroll
+        for (int r = 0; r < RL; r++) pc[r] = P.rl_pc[r];
+        constexpr int NT = RHS_LDS_MAX / WAVE;
+        double tv[RL][NT];
+#pragma unroll
+        for (int r = 0; r < RL; r++) {
+            const int qm = pc[r].nk > 0 ? pc[r].nk - 1 : 0;
+            const double *src = pc[r].nk > 0 ? P.rhs + pc[r].toff : P.alpha_pow;   // any valid pointer
+#pragma unroll
+            for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
+        }
+        Pcg g = P.cm.rng.load(el);
+#pragma unroll
+        for (int r = 0; r < RL; r++)
+#pragma unroll
+            for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
+        wave_lds_sync();
+        int t = t_start;
+        for (int c = 0; c < nch; c++) {
+            double *db = dbuf + (c & 1) * CH * RL * WAVE;
+            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+                if (t >= P.T) {                    // NEXT_STEP reset step: no draw
+                    t = 0;
+                    continue;
+                }
+                double Dd[RL];
+                spec_demand<G>(g, pc, rhs_l, Dd);
+#pragma unroll
+                for (int r = 0; r < RL; r++) db[(kk * RL + r) * WAVE + lane] = Dd[r];
+                t++;
+            }
+            net_wg_sync();   // barrier c: chunk c ready
+        }
+        if (valid) P.cm.rng.store_state(e, g);
+        return;
+    }
+    // ---- dynamics wave
+    float *trow = tile + lane * O;
+    int t = t_start;
+    NetSt<G> st;
+#pragma unroll
+    for (int j = 0; j < G::J; j++) st.X[j] = P.X[j * S + el];
+#pragma unroll
+    for (int r = 0; r < RL; r++) st.U[r] = P.U[r * S + el];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) st.Y[k] = P.Y[k * S + el];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+        if (G::L[k] == 0) continue;
+#pragma unroll
+        for (int a = 1; a <= G::L[k]; a++) {
+            const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+            const double v = P.Rring[(int64_t)row * S + el];
+            st.w[G::ring_off[k] + a - 1] = (t - a >= 0) ? v : 0.0;   // zeroed history (:315-321)
+        }
+    }
+    float nact[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) nact[k] = io.act[el * G::E + k];
+    double napow = P.alpha_pow[t < P.T ? t : 0];
+    double dlast[RL];
+#pragma unroll
+    for (int r = 0; r < RL; r++) dlast[r] = 0.0;
+    bool last_real = false;
+    double Rn[G::E];
+    net_wg_sync();   // barrier 0: chunk 0 ready
+    for (int c = 0; c < nch; c++) {
+        const double *db = dbuf + (c & 1) * CH * RL * WAVE;
+        for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+            const int k = c * CH + kk;
+            const int64_t oi = (int64_t)k * N + e;
+            float act[G::E];
+#pragma unroll
+            for (int q = 0; q < G::E; q++) act[q] = nact[q];
+            const double apow = napow;
+            {
+                const int tn = (t >= P.T) ? 0 : t + 1;          // the next launch step's period
+                napow = P.alpha_pow[tn < P.T ? tn : 0];
+            }
+            if (k + 1 < K) {                                    // the next step's actions
+#pragma unroll
+                for (int q = 0; q < G::E; q++) nact[q] = io.act[((int64_t)(k + 1) * N + el) * G::E + q];
+            }
+            if (t >= P.T) {                                     // NEXT_STEP autoreset (:301-332)
+                spec_reset<G>(st, trow);
+                if (valid) {
+                    out_store(io.rew + oi, 0.0);
+                    out_store(io.term + oi, (uint8_t)0);
+                    out_store(io.trunc + oi, (uint8_t)0);
+                }
+                t = 0;
+            } else {
+                double Dd[RL];
+#pragma unroll
+                for (int r = 0; r < RL; r++) Dd[r] = db[(kk * RL + r) * WAVE + lane];
+                const double rw = spec_dyn<G>(P, t, apow, st, act, Dd, trow, Rn, nullptr, nullptr);
+                if (valid) {
+                    out_store(io.rew + oi, rw);
+                    out_store(io.term + oi, (uint8_t)0);
+                    out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.T ? 1 : 0));
+                }
+                spec_shift<G>(st, Rn);
+#pragma unroll
+                for (int r = 0; r < RL; r++) dlast[r] = Dd[r];
+                last_real = k == K - 1;
+                t += 1;
+            }
+            wave_lds_sync();
+            store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+            wave_lds_sync();
+        }
+        if (c + 1 < nch) net_wg_sync();   // barrier c + 1
+    }
+    if (valid) {
+#pragma unroll
+        for (int j = 0; j < G::J; j++) st_store(P.X + j * S + e, st.X[j]);
+#pragma unroll
+        for (int r = 0; r < RL; r++) st_store(P.U + r * S + e, st.U[r]);
+#pragma unroll
+        for (int k = 0; k < G::E; k++) st_store(P.Y + k * S + e, st.Y[k]);
+        // ring slot of R[t - a] = age-a window register (zeros before the episode)
+#pragma unroll
+        for (int k = 0; k < G::E; k++) {
+            if (G::L[k] == 0) continue;
+#pragma unroll
+            for (int a = 1; a <= G::L[k]; a++)
+                st_store(P.Rring + (int64_t)(G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k])) * S + e,
+                         st.w[G::ring_off[k] + a - 1]);
+        }
+        if (P.cm.info_demand && last_real) {
+#pragma unroll
+            for (int r = 0; r < RL; r++) P.cm.info_demand[e * RL + r] = (int64_t)dlast[r];
+        }
+    }
+}
+
 }  // namespace
 
 template <class G>
@@ -440,6 +648,12 @@ int net_spec_match(const invsim_netinvmgmt_spec &h) {
     return NET_SPEC_NONE;
 }
 
+// INVSIM_NET_ROLL=0 keeps rollouts on net_spec_kernel (A/B measurements, tests)
+static bool net_roll_enabled() {
+    const char *v = getenv("INVSIM_NET_ROLL");
+    return !(v && v[0] == '0');
+}
+
 template <class G>
 static size_t spec_lds_bytes() {
     return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float) + (size_t)G::RL * RHS_LDS_MAX * sizeof(double);
@@ -453,6 +667,12 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
 #define K_(TU, ONE, POL) hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
+    if (!pol && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
+        (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
+        const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE)), br(2 * WAVE);
+        hipLaunchKernelGGL((net_roll_kernel<G>), gr, br, NetRoll<G>::lds(), s, p, t_u, io);
+        return hipGetLastError();
+    }
     if (pol) {
         if (t_u >= 0) K_(true, false, true);
         else K_(false, false, true);

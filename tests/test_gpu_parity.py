@@ -687,3 +687,45 @@ def test_invmgmt_register_window_rollout_equals_one_wave(gpu, monkeypatch, cls, 
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
     monkeypatch.delenv("INVSIM_IM_ROLL")
+
+
+@pytest.mark.parametrize("graph,backlog,n,pre,Ks,mode", [
+    ("default", True, 4000, 0, (75, 2, 9), "next_step"),
+    ("default", False, 1000, 7, (40, 16, 3), "next_step"),
+    ("custom", True, 3000, 5, (61, 8), "next_step"),
+    ("default", True, 32768, 3, (33,), "next_step"),
+    ("default", True, 1000, 5, (8, 17), "disabled"),
+])
+def test_net_demand_wave_rollout_equals_one_wave(gpu, monkeypatch, graph, backlog, n, pre, Ks, mode):
+    """invsim_rollout of a compiled network runs net_roll_kernel (demand wave +
+    actions loaded a step ahead); INVSIM_NET_ROLL=0 keeps it on
+    net_spec_kernel.  Both paths from the same state: identical outputs,
+    demand record and state."""
+    import invsim
+    from invsim.topology import custom_graph, default_graph
+    mk_g = default_graph if graph == "default" else custom_graph
+    envs = []
+    for i in range(2):
+        env = invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), backlog=backlog, autoreset_mode=mode,
+                                         record_demand=True)
+        env.reset(seed=41)
+        envs.append(env)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(9)
+    A = envs[0].action_dim
+    for k in range(pre):
+        a = torch.rand((n, A), device=gpu, generator=g) * 250
+        for env in envs:
+            env.step(a)
+    for K in Ks:
+        a = torch.rand((K, n, A), device=gpu, generator=g) * 260 - 5
+        outs, dems = [], []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_NET_ROLL", "1" if i == 0 else "0")
+            outs.append(env.rollout(a))
+            dems.append(env._demand.clone())
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), K
+        assert torch.equal(dems[0], dems[1])
+        assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
+    monkeypatch.delenv("INVSIM_NET_ROLL")
