@@ -608,6 +608,191 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
     }
 }
 
+// numpy random_poisson's constants of a per-env rate, computed once per episode
+// (np_poisson_dyn recomputes them per draw)
+__device__ __forceinline__ PtrsConst nv_rate_const(double lam) {
+    PtrsConst c;
+    c.lam = lam;
+    c.slam = sqrt(lam);
+    c.loglam = log(lam);
+    c.b = 0.931 + 2.53 * c.slam;
+    c.a = -0.059 + 0.02483 * c.b;
+    c.invalpha = 1.1239 + 1.1328 / (c.b - 3.4);
+    c.vr = 0.9277 - 3.6224 / (c.b - 2);
+    c.log_invalpha = log(c.invalpha);
+    c.a2 = 2 * c.a;
+    c.enlam = exp(-lam);
+    c.k0 = 0;
+    c.nk = 0;
+    return c;
+}
+
+// np_poisson_dyn with the episode's constants (same draws, same arithmetic)
+__device__ __forceinline__ int64_t nv_poisson_c(Pcg &g, const PtrsConst &c, const double *lgtab) {
+    if (c.lam >= 10) return np_poisson_ptrs_lg(g, c, lgtab, RHS_LDS_MAX);
+    if (c.lam == 0) return 0;
+    return np_poisson_mult(g, c.enlam);
+}
+
+__device__ __forceinline__ void nv_wg_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// K-step lock-step rollout (invsim_rollout without a policy, NEXT_STEP or
+// DISABLED autoreset, compile-time lead time LT > 0), one 128-thread workgroup
+// per 64 envs:
+//   wave 0 (stream)   owns every env's generator: draws the demands of up to CH
+//                     launch steps ahead into a double-buffered LDS ring with
+//                     the episode's Poisson constants kept in registers, and
+//                     runs the reset draws (5 uniforms -> price, cost, h, k, mu,
+//                     newsvendor.py:100-123), handing the new params over in
+//                     LDS.  A demand depends on the stream and mu only.
+//   wave 1 (dynamics) the step (newsvendor.py:125-204) with the pipeline in
+//                     registers; its action is loaded a step ahead, before the
+//                     previous step's stores (vmcnt is in order).
+// A chunk ends after CH steps or after a reset step, so it carries at most one
+// set of new params.  Both waves derive the same chunk boundaries from the
+// lock-step period.  Chunk handoff as im_roll3_kernel: wave 0 fills buffer
+// c & 1, barrier c, wave 1 consumes chunk c after barrier c.
+template <int LT>
+struct NvRoll {
+    static constexpr int CH = 8;
+    static constexpr int O = LT + 5;
+    static constexpr size_t tile_bytes() { return (size_t)((EPW * O + 3) / 4) * 4 * sizeof(float); }
+    static constexpr size_t lds() {
+        return tile_bytes() + RHS_LDS_MAX * sizeof(double) + 2 * (size_t)CH * WAVE * sizeof(int64_t) +
+               2 * 5 * (size_t)WAVE * sizeof(double);
+    }
+};
+
+template <int LT>
+__global__ void __launch_bounds__(2 * WAVE)
+nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
+    using R = NvRoll<LT>;
+    constexpr int O = R::O, CH = R::CH;
+    constexpr int TILE_IT = (EPW * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
+    extern __shared__ __attribute__((aligned(16))) float nr_lds[];
+    float *tile = nr_lds;
+    double *lg_l = reinterpret_cast<double *>(nr_lds + R::tile_bytes() / sizeof(float));
+    int64_t *dbuf = reinterpret_cast<int64_t *>(lg_l + RHS_LDS_MAX);     // [2][CH][WAVE]
+    double *pbuf = reinterpret_cast<double *>(dbuf + 2 * CH * WAVE);      // [2][5][WAVE]
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e = e0 + lane;
+    const bool valid = e < N;
+    const int64_t el = valid ? e : N - 1;       // padded lanes: the last env's data, never stored
+    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
+    const int K = io.K;
+    const bool nxt = P.cm.autoreset == AR_NEXT_STEP;
+    if (threadIdx.x < WAVE) {   // ---- stream wave
+        TableStage ts;
+        ts.dst = lg_l;
+        ts.load(P.lgtab, RHS_LDS_MAX, lane);
+        NvState<LT> st;
+        st.g = P.cm.rng.load(el);
+        PtrsConst c = nv_rate_const(P.par[4 * S + el]);
+        ts.flush(lane);
+        bool reset_any = false;
+        int t = t_start, kk = 0, cb = 0;
+        for (int k = 0; k < K; k++) {
+            const bool rs = nxt && t >= P.step_limit;
+            if (rs) {                              // reset(): 5 uniforms (:105-111)
+                nv_reset_regs<LT>(P, e, st, nullptr, false);
+#pragma unroll
+                for (int j = 0; j < 5; j++) pbuf[(cb * 5 + j) * WAVE + lane] = st.par[j];
+                c = nv_rate_const(st.par[4]);
+                reset_any = true;
+                t = 0;
+            } else {
+                dbuf[(cb * CH + kk) * WAVE + lane] = nv_poisson_c(st.g, c, lg_l);   // :146
+                t++;
+            }
+            if (++kk == CH || rs || k == K - 1) {  // chunk closes
+                nv_wg_sync();
+                kk = 0;
+                cb ^= 1;
+            }
+        }
+        if (valid) {
+            P.cm.rng.store_state(e, st.g);
+            if (reset_any) {
+#pragma unroll
+                for (int j = 0; j < 5; j++) P.par[j * S + e] = st.par[j];
+            }
+        }
+        return;
+    }
+    // ---- dynamics wave
+    float *trow = tile + lane * O;
+    NvState<LT> st;
+    int sc = t_start;
+#pragma unroll
+    for (int j = 0; j < 5; j++) st.par[j] = P.par[j * S + el];
+    {
+        const int base = (int)((uint32_t)(sc + 1) % (uint32_t)LT);
+#pragma unroll
+        for (int p = 0; p < LT; p++) {
+            int sl = base + p;
+            sl = sl >= LT ? sl - LT : sl;
+            st.pv[p] = P.pipe[(int64_t)sl * S + el];
+            if (!(p >= LT - sc)) st.pv[p] = 0.f;
+        }
+    }
+    float nact = io.act[el];
+    int kk = 0, cb = 0;
+    nv_wg_sync();   // barrier 0: chunk 0 ready
+    for (int k = 0; k < K; k++) {
+        const int64_t oi = (int64_t)k * N + e;
+        const float act = nact;
+        if (k + 1 < K) nact = io.act[(int64_t)(k + 1) * N + el];   // the next step's action
+        const bool rs = nxt && sc >= P.step_limit;
+        if (rs) {                                                  // NEXT_STEP autoreset
+#pragma unroll
+            for (int j = 0; j < 5; j++) st.par[j] = pbuf[(cb * 5 + j) * WAVE + lane];
+#pragma unroll
+            for (int p = 0; p < LT; p++) st.pv[p] = 0.f;
+            obs_params(st.par, trow);
+#pragma unroll
+            for (int j = 0; j < LT; j++) trow[5 + j] = 0.f;
+            if (valid) {
+                out_store(io.rew + oi, 0.0);
+                out_store(io.term + oi, (uint8_t)0);
+                out_store(io.trunc + oi, (uint8_t)0);
+            }
+            sc = 0;
+        } else {
+            const int64_t d = dbuf[(cb * CH + kk) * WAVE + lane];
+            double r;
+            const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, lg_l, nullptr, r,
+                                             (valid && k == K - 1) ? P.cm.info_demand : nullptr, d);
+            if (valid) {
+                out_store(io.rew + oi, r);
+                out_store(io.term + oi, (uint8_t)0);
+                out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
+            }
+            sc += 1;
+        }
+        wave_lds_sync();
+        store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+        wave_lds_sync();
+        if (++kk == CH || rs || k == K - 1) {      // chunk consumed
+            if (k + 1 < K) nv_wg_sync();             // barrier of the next chunk
+            kk = 0;
+            cb ^= 1;
+        }
+    }
+}
+
+// INVSIM_NV_ROLL=0 keeps rollouts on nv_run_kernel (A/B measurements, tests)
+inline bool nv_roll_enabled() {
+    const char *v = getenv("INVSIM_NV_ROLL");
+    return !(v && v[0] == '0');
+}
+
 // cm.rng <- the committed slot of the lookahead cache
 __global__ void __launch_bounds__(256) nv_commit_kernel(NvParams P, int slot) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -701,6 +886,18 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
         const hipError_t ce = nv_commit_launch(p, slot, s);
         ahead = false;
         if (ce != hipSuccess) return ce;
+    }
+    if (!pol && io.K > 1 && t_u >= 0 && p.L > 0 && p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
+        const dim3 gr(grid_for(p.cm.N, WAVE)), br(2 * WAVE);
+        bool done = true;
+#define R_(X)                                                                                              \
+    do {                                                                                                   \
+        if (X > 0) hipLaunchKernelGGL((nv_roll_kernel<(X > 0 ? X : 1)>), gr, br, NvRoll<(X > 0 ? X : 1)>::lds(), s, p, t_u, io); \
+        else done = false;                                                                                 \
+    } while (0)
+        NV_LT_SWITCH(R_)
+#undef R_
+        if (done) return hipGetLastError();
     }
 #define K_(X, TU, ONE, POL) \
     hipLaunchKernelGGL((nv_run_kernel<X, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)

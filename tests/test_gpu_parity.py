@@ -729,3 +729,43 @@ def test_net_demand_wave_rollout_equals_one_wave(gpu, monkeypatch, graph, backlo
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
     monkeypatch.delenv("INVSIM_NET_ROLL")
+
+
+@pytest.mark.parametrize("L,step_limit,n,pre,Ks,mode", [
+    (5, 40, 4000, 0, (75, 2, 9), "next_step"),
+    (5, 3, 1000, 1, (40, 17), "next_step"),      # several resets per demand chunk
+    (1, 7, 3000, 5, (61, 8), "next_step"),
+    (9, 40, 65536, 3, (45,), "next_step"),
+    (16, 10, 777, 2, (30,), "next_step"),
+    (5, 12, 1000, 5, (8, 17), "disabled"),       # stepping past step_limit
+])
+def test_newsvendor_stream_wave_rollout_equals_one_wave(gpu, monkeypatch, L, step_limit, n, pre, Ks, mode):
+    """invsim_rollout of Newsvendor runs nv_roll_kernel (stream wave drawing
+    demands and reset params ahead, action loaded a step ahead);
+    INVSIM_NV_ROLL=0 keeps it on nv_run_kernel.  Same state in, identical
+    outputs, demand record and state out."""
+    import invsim
+    envs = []
+    for i in range(2):
+        env = invsim.NewsvendorEnv(n, device=gpu, lead_time=L, step_limit=step_limit, autoreset_mode=mode,
+                                   record_demand=True)
+        env.reset(seed=41)
+        envs.append(env)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(9)
+    for k in range(pre):
+        a = torch.rand((n, 1), device=gpu, generator=g) * 400
+        for env in envs:
+            env.step(a)
+    for K in Ks:
+        a = torch.rand((K, n, 1), device=gpu, generator=g) * 2600 - 100
+        outs, dems = [], []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_NV_ROLL", "1" if i == 0 else "0")
+            outs.append(env.rollout(a))
+            dems.append(env._demand.clone())
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), K
+        assert torch.equal(dems[0], dems[1])
+        assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
+    monkeypatch.delenv("INVSIM_NV_ROLL")
