@@ -931,7 +931,11 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                     t = 0;
                     continue;
                 }
+#ifdef INVSIM_ABL_ROLL_NO_DRAW
+                int64_t d = 20;
+#else
                 int64_t d = env_poisson(g, P.pc, rhs_l);                // :280
+#endif
                 db[kk * WAVE + lane] = d < 0 ? 0 : d;
                 t++;
             }
@@ -1109,8 +1113,10 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 t += 1;
             }
             wave_lds_sync();
+#ifndef INVSIM_ABL_ROLL_NO_STORE
             store_tile<(O * WAVE * 8 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + ((int64_t)k * N + e0) * O,
                                                                     (int64_t)nvalid * O, lane);
+#endif
             wave_lds_sync();
         }
         if (c + 1 < nch) wg_lds_sync();   // barrier c + 1

@@ -506,7 +506,11 @@ net_roll_kernel(NetParams P, int t_start, StepIO<float, float> io) {
                     continue;
                 }
                 double Dd[RL];
+#ifdef INVSIM_ABL_ROLL_NO_DRAW
+                for (int r = 0; r < RL; r++) Dd[r] = 20.0;
+#else
                 spec_demand<G>(g, pc, rhs_l, Dd);
+#endif
 #pragma unroll
                 for (int r = 0; r < RL; r++) db[(kk * RL + r) * WAVE + lane] = Dd[r];
                 t++;
@@ -588,7 +592,9 @@ net_roll_kernel(NetParams P, int t_start, StepIO<float, float> io) {
                 t += 1;
             }
             wave_lds_sync();
+#ifndef INVSIM_ABL_ROLL_NO_STORE
             store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+#endif
             wave_lds_sync();
         }
         if (c + 1 < nch) net_wg_sync();   // barrier c + 1

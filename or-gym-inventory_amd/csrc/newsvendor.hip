@@ -708,7 +708,11 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
                 reset_any = true;
                 t = 0;
             } else {
+#ifdef INVSIM_ABL_ROLL_NO_DRAW
+                dbuf[(cb * CH + kk) * WAVE + lane] = 20;
+#else
                 dbuf[(cb * CH + kk) * WAVE + lane] = nv_poisson_c(st.g, c, lg_l);   // :146
+#endif
                 t++;
             }
             if (++kk == CH || rs || k == K - 1) {  // chunk closes
@@ -777,7 +781,9 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
             sc += 1;
         }
         wave_lds_sync();
+#ifndef INVSIM_ABL_ROLL_NO_STORE
         store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+#endif
         wave_lds_sync();
         if (++kk == CH || rs || k == K - 1) {      // chunk consumed
             if (k + 1 < K) nv_wg_sync();             // barrier of the next chunk
