@@ -17,7 +17,8 @@ RCCL (the only cross-GPU exchange the path has).
 Prints ONE JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per
 launch (SURVEY §8(d) B1 x N) / mean kernel time from HIP events on the stream
 the kernel runs on.  `cpu_baseline` = the C oracle (a single-thread port of the
-reference step) timed on this host on a bounded sample.
+reference step, env loop OpenMP-parallel over up to 16 host cores; the
+single-thread rate beside it) timed on this host on a bounded sample.
 """
 import argparse
 import json
@@ -56,7 +57,7 @@ def parse():
     ap.add_argument("--rollout-k", type=int, default=30)
     ap.add_argument("--n-envs", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--pool", type=int, default=16, help="distinct action batches cycled")
     return ap.parse_args()
 
@@ -73,13 +74,20 @@ def make_actions(env, pool, K, gen):
     return torch.rand(shape, device=env.device, generator=gen) * hi
 
 
-def cpu_baseline(wl, seconds):
-    """C oracle (single-thread restatement of the reference step) on this host."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _oracle_rate(pyoracle, wl, n, threads, seconds):
+    """env-steps/s of the C oracle over whole episodes (resets included)."""
     import numpy as np
-    import pyoracle
-    pyoracle.build()
-    n = 8192
+    pyoracle.set_threads(threads)
     rng = np.random.default_rng(0)
     if wl["cls"].startswith("InvManagement"):
         env = pyoracle.OracleInvMgmt(n, backlog=wl["cls"].endswith("BacklogEnv"))
@@ -105,9 +113,30 @@ def cpu_baseline(wl, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return dict(value=steps / el, unit="env-steps/s", cores=1, kind="port",
-                sample=f"{n} envs x {steps // n} steps ({steps // n // T} episodes incl. resets), "
-                       f"oracle/oracle.c single thread, {el:.1f} s")
+    pyoracle.set_threads(1)
+    return steps / el, steps // n, el
+
+
+def cpu_baseline(wl, seconds):
+    """C oracle (restatement of the reference step, env loop parallel over the
+    host's cores with OpenMP) on this host; the single-thread rate beside it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    pyoracle.build()
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))        # the box's CPU share per GPU is 16
+    n1 = 8192
+    nT = 32768 if wl["cls"].startswith("NetInvMgmt") else 65536
+    v1, s1, e1 = _oracle_rate(pyoracle, wl, n1, 1, seconds / 2)
+    vT, sT, eT = _oracle_rate(pyoracle, wl, nT, threads, seconds / 2)
+    return dict(value=vT, unit="env-steps/s", cores=threads, kind="port",
+                sample=f"{nT} envs x {sT} steps ({sT // (40 if wl['cls'] == 'NewsvendorEnv' else 30)} episodes "
+                       f"incl. resets), oracle/oracle.c OpenMP {threads} threads, {eT:.1f} s",
+                single_thread={"value": v1, "sample": f"{n1} envs x {s1} steps, 1 thread, {e1:.1f} s"},
+                cpu_model=_cpu_model(), host_cpus_visible=cores)
 
 
 def main():

@@ -345,6 +345,22 @@ int64_t orc_binomial(uint64_t rng[4], int64_t n, double p) {
 }
 
 #include "numpy_ziggurat.h"
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* Env-parallel batch loops (each env owns its generator and history, so the
+ * results do not depend on the thread count).  Default 1 thread: the tests use
+ * the oracle as a checker; bench.py's cpu_baseline sets the host's cores. */
+static int orc_threads = 1;
+void orc_set_threads(int n) { orc_threads = n > 0 ? n : 1; }
+int orc_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_num_procs();
+#else
+    return 1;
+#endif
+}
 
 /* random_standard_exponential (256-level ziggurat, tables from numpy) */
 double orc_standard_exponential(uint64_t rng[4]) {
@@ -524,6 +540,7 @@ void orc_nv_seed(void *p, const uint32_t *words, const int32_t *nwords) {
 void orc_nv_reset(void *p, float *obs) {
     nv_t *h = (nv_t *)p;
     const int O = h->c.lead_time + 5;
+#pragma omp parallel for schedule(static) num_threads(orc_threads)
     for (int64_t i = 0; i < h->n; i++) {
         uint64_t *rng = h->rng + 4 * i;
         double *par = h->par + 5 * i;
@@ -568,6 +585,7 @@ void orc_nv_step(void *p, const float *action, float *obs, double *reward, uint8
     const int L = h->c.lead_time;
     const int O = L + 5;
     const tv ZERO = tv_make(0.0, K_PY);
+#pragma omp parallel for schedule(static) num_threads(orc_threads)
     for (int64_t i = 0; i < h->n; i++) {
         uint64_t *rng = h->rng + 4 * i;
         const double *par = h->par + 5 * i;
@@ -701,6 +719,7 @@ static void im_obs(im_t *h, int64_t i, int64_t *obs) {
 void orc_im_reset(void *p, int64_t *obs) {
     im_t *h = (im_t *)p;
     const int m1 = h->m1, m = h->m;
+#pragma omp parallel for schedule(static) num_threads(orc_threads)
     for (int64_t i = 0; i < h->n; i++) {
         int64_t *I = h->I + (int64_t)i * (h->T + 1) * m1;
         memset(I, 0, sizeof(int64_t) * (h->T + 1) * m1);
@@ -730,6 +749,7 @@ void orc_im_step(void *p, const int64_t *action, int64_t *obs, double *reward, u
                  int64_t *backlog_next) {
     im_t *h = (im_t *)p;
     const int m1 = h->m1, m = h->m;
+#pragma omp parallel for schedule(static) num_threads(orc_threads)
     for (int64_t i = 0; i < h->n; i++) {
         uint64_t *rng = h->rng + 4 * i;
         const int t = h->period[i];
@@ -922,6 +942,7 @@ static void net_obs(net_t *h, int64_t i, float *obs) {
 void orc_net_reset(void *p, float *obs) {
     net_t *h = (net_t *)p;
     const int E = h->E ? h->E : 1, RLs = h->RL ? h->RL : 1;
+#pragma omp parallel for schedule(static) num_threads(orc_threads)
     for (int64_t i = 0; i < h->n; i++) {
         memset(NX(h, i), 0, sizeof(double) * (h->T + 2) * h->J);
         memset(NY(h, i), 0, sizeof(double) * (h->T + 2) * E);
@@ -944,6 +965,7 @@ void orc_net_step(void *p, const float *action, float *obs, double *reward, uint
     const int J = h->J, EE = h->E, RL = h->RL;
     const int E = EE ? EE : 1, RLs = RL ? RL : 1, SL = h->E + h->RL + 1;
     double cons[64], arr[64], xb[64], prof[64];
+#pragma omp parallel for schedule(static) num_threads(orc_threads) private(cons, arr, xb, prof)
     for (int64_t i = 0; i < h->n; i++) {
         uint64_t *rng = h->rng + 4 * i;
         const int t = h->period[i];

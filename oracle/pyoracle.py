@@ -52,6 +52,8 @@ def _lib():
     lib.orc_sum_f32.restype = C.c_float
     lib.orc_sum_f64.argtypes = [P, C.c_int64]
     lib.orc_sum_f64.restype = C.c_double
+    lib.orc_set_threads.argtypes = [C.c_int]
+    lib.orc_max_threads.restype = C.c_int
     for fam in ("nv", "im", "net"):
         getattr(lib, f"orc_{fam}_create").argtypes = [P, C.c_int64]
         getattr(lib, f"orc_{fam}_create").restype = P
@@ -68,6 +70,15 @@ def _lib():
 
 
 LIB = None
+
+
+def set_threads(n):
+    """Threads of the oracle's env-parallel batch loops (OpenMP; default 1)."""
+    lib().orc_set_threads(int(n))
+
+
+def max_threads():
+    return int(lib().orc_max_threads())
 
 
 def lib():

@@ -220,3 +220,31 @@ def test_oracle_invmgmt_demand_stream_is_numpys(oracle, dist, dp):
         else:
             e = [g.geometric(dp["p"]) for _ in range(60)]
         assert np.array_equal(dem[i], np.maximum(np.array(e), 0)), i
+
+
+@pytest.mark.parametrize("fam", ["nv", "im", "net"])
+def test_oracle_thread_count_independent(oracle, fam):
+    """The OpenMP env loop (bench.py's multi-core cpu_baseline) gives the same
+    trajectories as the single-thread loop."""
+    n, T = 301, 12
+    outs = []
+    for threads in (1, 4):
+        oracle.set_threads(threads)
+        rng = np.random.default_rng(3)
+        if fam == "nv":
+            env = oracle.OracleNewsvendor(n)
+            acts = [rng.uniform(0, 400, size=n).astype(np.float32) for _ in range(T)]
+        elif fam == "im":
+            env = oracle.OracleInvMgmt(n, backlog=True)
+            acts = [rng.integers(0, 231, size=(n, 3)).astype(np.int64) for _ in range(T)]
+        else:
+            env = oracle.OracleNet(n)
+            acts = [rng.uniform(0, 200, size=(n, 11)).astype(np.float32) for _ in range(T)]
+        env.seed(range(5, 5 + n))
+        rec = [env.reset()]
+        for a in acts:
+            rec.extend(np.asarray(x).copy() for x in env.step(a)[:3])
+        outs.append(rec)
+    oracle.set_threads(1)
+    for x, y in zip(*outs):
+        assert np.array_equal(x.view(np.uint8), y.view(np.uint8))

@@ -11,6 +11,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROLL_KERNELS = {"invmgmt_backlog": "im_roll3_kernel", "invmgmt_lostsales": "im_roll3_kernel",
+                "newsvendor": "nv_roll_kernel", "net_backlog": "net_roll_kernel"}
 KERNELS = {"invmgmt_backlog": "im_split_kernel", "invmgmt_lostsales": "im_split_kernel",
            "newsvendor": "nv_step1_kernel", "net_backlog": "net_spec_kernel"}
 
@@ -21,6 +23,17 @@ def last_json(path):
     for line in reversed(open(path).read().splitlines()):
         if line.startswith("{"):
             return json.loads(line)
+    return None
+
+
+def kernel_avg_ns(csv_path, kern):
+    """Average duration (ns) of the named kernel in a rocprofv3 kernel_stats.csv."""
+    import csv
+    if not os.path.exists(csv_path):
+        return None
+    for row in csv.DictReader(open(csv_path)):
+        if kern in row["Name"]:
+            return float(row["AverageNs"])
     return None
 
 
@@ -36,6 +49,9 @@ def main():
         if os.path.isdir(prof):
             shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"),
                         os.path.join(dst, f"{wl}_step_kernel_stats.csv"))
+            roll = os.path.join(prof, "trace_roll", "run_kernel_stats.csv")
+            if os.path.exists(roll):
+                shutil.copy(roll, os.path.join(dst, f"{wl}_rollout_kernel_stats.csv"))
             subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), prof, wl, kern,
                             os.path.join(dst, f"pmc_{wl}.json")], check=True, capture_output=True)
         for mode in ("step", "rollout"):
@@ -51,7 +67,8 @@ def main():
                         f"{r['kernel_ms_mean'] * 1e3:.2f} | {r['bytes_per_env_step']:.0f} | {r['achieved']:.0f} | "
                         f"{r['frac']:.3f} | "
                         + (f"{pm['rocprof_kernel_ns_mean'] / 1e3:.2f} | {pm['traffic_over_algorithmic']:.2f} |"
-                           if pm else " | |"))
+                           if pm else
+                           f"{(kernel_avg_ns(os.path.join(dst, f'{wl}_rollout_kernel_stats.csv'), ROLL_KERNELS[wl]) or float('nan')) / 1e3:.2f} | |"))
     d = last_json(os.path.join(src, "bench_default.log"))
     if d:
         with open(os.path.join(dst, "bench_default.json"), "w") as f:
@@ -59,7 +76,7 @@ def main():
     with open(os.path.join(dst, "SUMMARY.md"), "w") as f:
         f.write(f"# Round {rnd} measurements (gpurun_out/round_{tag}, 1x MI355X)\n\n")
         f.write("| workload | mode | envs | env-steps/s | kernel µs/launch (events) | B/env-step | "
-                "achieved GB/s | frac of 8 TB/s | rocprof µs (step) | PMC traffic / algorithmic |\n")
+                "achieved GB/s | frac of 8 TB/s | rocprof µs/launch | PMC traffic / algorithmic |\n")
         f.write("|---|---|---|---|---|---|---|---|---|---|\n")
         f.write("\n".join(rows) + "\n")
     print(open(os.path.join(dst, "SUMMARY.md")).read())

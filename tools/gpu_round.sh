@@ -36,6 +36,8 @@ for part in $PARTS; do
       P=$OUT/prof_$w
       run timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -o run -- \
           python bench.py --workload $w --steps 1000 --warmup 50 --no-cpu-baseline > $P.trace.log 2>&1
+      run timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace_roll -o run -- \
+          python bench.py --workload $w --mode rollout --steps 600 --warmup 60 --no-cpu-baseline > $P.trace_roll.log 2>&1
       run timeout -k 10 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/pmc_fetch -o run -- \
           python bench.py --workload $w --steps 200 --warmup 20 --no-cpu-baseline > $P.fetch.log 2>&1
       run timeout -k 10 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/pmc_write -o run -- \
