@@ -640,45 +640,71 @@ __device__ __forceinline__ void nv_wg_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// numpy's sampler branch of a rate: true = the multiplication method (0 < lam < 10;
+// like nv_poisson_c, anything not >= 10 and not 0 -- NaN included -- goes there)
+__device__ __forceinline__ bool nv_mult_branch(double lam) { return !(lam >= 10) && lam != 0; }
+
+// Launch-step chunks of the rollout: a chunk ends after CH steps, at a reset
+// step (NEXT_STEP, period >= step_limit: the chunk's last step), or at the end
+// of the launch.  Every wave derives the same chunks from the lock-step period.
+__device__ __forceinline__ void nv_chunk(int t, int rem, int step_limit, bool nxt, int ch, int &len, bool &rs) {
+    len = 0;
+    rs = false;
+    while (len < ch && len < rem) {
+        len++;
+        if (nxt && t >= step_limit) {
+            rs = true;
+            break;
+        }
+        t++;
+    }
+}
+
 // K-step lock-step rollout (invsim_rollout without a policy, NEXT_STEP or
-// DISABLED autoreset, compile-time lead time LT > 0), one 128-thread workgroup
+// DISABLED autoreset, compile-time lead time LT > 0), one 192-thread workgroup
 // per 64 envs:
-//   wave 0 (stream)   owns every env's generator: draws the demands of up to CH
-//                     launch steps ahead into a double-buffered LDS ring with
-//                     the episode's Poisson constants kept in registers, and
-//                     runs the reset draws (5 uniforms -> price, cost, h, k, mu,
-//                     newsvendor.py:100-123), handing the new params over in
-//                     LDS.  A demand depends on the stream and mu only.
-//   wave 1 (dynamics) the step (newsvendor.py:125-204) with the pipeline in
-//                     registers; its action is loaded a step ahead, before the
-//                     previous step's stores (vmcnt is in order).
-// A chunk ends after CH steps or after a reset step, so it carries at most one
-// set of new params.  Both waves derive the same chunk boundaries from the
-// lock-step period.  Chunk handoff as im_roll3_kernel: wave 0 fills buffer
-// c & 1, barrier c, wave 1 consumes chunk c after barrier c.
+//   wave 0 (PTRS stream)  draws the demands (newsvendor.py:146) of the envs whose
+//   wave 1 (mult stream)  rate takes numpy's PTRS branch (lam >= 10, or 0) /
+//                         multiplication branch (0 < lam < 10) for the next chunk
+//                         of launch steps into a double-buffered LDS ring, with
+//                         the episode's Poisson constants in registers.  A lane
+//                         works through its chunk's draws without waiting for
+//                         the other lanes' rejections (one flat loop).  The
+//                         branch owning an env's generator runs its reset draws
+//                         (5 uniforms -> price, cost, h, k, mu, :100-123) and
+//                         hands params and generator state over in LDS; the
+//                         branch of the new rate owns it next.
+//   wave 2 (dynamics)     the step (:125-204) with the pipeline in registers;
+//                         its action is loaded a step ahead, before the previous
+//                         step's stores (vmcnt is in order).
+// A chunk carries at most one reset (its last step).  Handoff: the stream waves
+// fill buffer c & 1, barrier c, the dynamics wave consumes chunk c after
+// barrier c.  Same draws, same order, same arithmetic as nv_run_kernel.
 template <int LT>
 struct NvRoll {
     static constexpr int CH = 8;
     static constexpr int O = LT + 5;
+    static constexpr int NP = 7;   // reset handoff: price, cost, h, k, mu, state hi, state lo
     static constexpr size_t tile_bytes() { return (size_t)((EPW * O + 3) / 4) * 4 * sizeof(float); }
     static constexpr size_t lds() {
         return tile_bytes() + RHS_LDS_MAX * sizeof(double) + 2 * (size_t)CH * WAVE * sizeof(int64_t) +
-               2 * 5 * (size_t)WAVE * sizeof(double);
+               2 * NP * (size_t)WAVE * sizeof(double);
     }
 };
 
 template <int LT>
-__global__ void __launch_bounds__(2 * WAVE)
+__global__ void __launch_bounds__(3 * WAVE)
 nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
     using R = NvRoll<LT>;
-    constexpr int O = R::O, CH = R::CH;
+    constexpr int O = R::O, CH = R::CH, NP = R::NP;
     constexpr int TILE_IT = (EPW * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
     extern __shared__ __attribute__((aligned(16))) float nr_lds[];
     float *tile = nr_lds;
     double *lg_l = reinterpret_cast<double *>(nr_lds + R::tile_bytes() / sizeof(float));
     int64_t *dbuf = reinterpret_cast<int64_t *>(lg_l + RHS_LDS_MAX);     // [2][CH][WAVE]
-    double *pbuf = reinterpret_cast<double *>(dbuf + 2 * CH * WAVE);      // [2][5][WAVE]
+    double *pbuf = reinterpret_cast<double *>(dbuf + 2 * CH * WAVE);      // [2][NP][WAVE]
     const int lane = threadIdx.x & (WAVE - 1);
+    const int role = threadIdx.x / WAVE;
     const int64_t N = P.cm.N;
     const int64_t S = P.cm.Npad;
     const int64_t e0 = (int64_t)blockIdx.x * WAVE;
@@ -688,42 +714,96 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
     const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
     const int K = io.K;
     const bool nxt = P.cm.autoreset == AR_NEXT_STEP;
-    if (threadIdx.x < WAVE) {   // ---- stream wave
+    if (role < 2) {   // ---- stream waves
+        const bool multw = role == 1;
         TableStage ts;
-        ts.dst = lg_l;
-        ts.load(P.lgtab, RHS_LDS_MAX, lane);
+        if (!multw) {
+            ts.dst = lg_l;
+            ts.load(P.lgtab, RHS_LDS_MAX, lane);
+        }
         NvState<LT> st;
         st.g = P.cm.rng.load(el);
         PtrsConst c = nv_rate_const(P.par[4 * S + el]);
-        ts.flush(lane);
+        bool mine = nv_mult_branch(c.lam) == multw;
+        if (!multw) ts.flush(lane);
         bool reset_any = false;
-        int t = t_start, kk = 0, cb = 0;
-        for (int k = 0; k < K; k++) {
-            const bool rs = nxt && t >= P.step_limit;
-            if (rs) {                              // reset(): 5 uniforms (:105-111)
+        int t = t_start, cb = 0;
+        for (int k0 = 0; k0 < K;) {
+            int len;
+            bool rs;
+            nv_chunk(t, K - k0, P.step_limit, nxt, CH, len, rs);
+            const int nd = mine ? len - (rs ? 1 : 0) : 0;    // draws of this lane (the reset step draws none)
+            int64_t *db = dbuf + cb * CH * WAVE + lane;
+#ifdef INVSIM_ABL_ROLL_NO_DRAW
+            for (int j = 0; j < nd; j++) db[j * WAVE] = 20;
+#else
+            if (!multw) {
+                if (c.lam == 0) {
+                    for (int j = 0; j < nd; j++) db[j * WAVE] = 0;
+                } else {
+                    // numpy random_poisson_ptrs, one trial per iteration, lanes independent
+                    for (int j = 0; j < nd;) {
+                        const double U = st.g.next_double() - 0.5;
+                        const double V = st.g.next_double();
+                        const double us = 0.5 - fabs(U);
+                        const int64_t kd = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+                        bool acc = (us >= 0.07) && (V <= c.vr);
+                        if (!acc && !((kd < 0) || ((us < 0.013) && (V > us)))) {
+                            const double r = (kd < RHS_LDS_MAX)
+                                                 ? (-c.lam + (double)kd * c.loglam) - lg_l[kd < RHS_LDS_MAX ? kd : 0]
+                                                 : -c.lam + (double)kd * c.loglam - np_loggam((double)(kd + 1));
+                            acc = ptrs_log_accept(c, V, us, r);
+                        }
+                        if (acc) {
+                            db[j * WAVE] = kd;
+                            j++;
+                        }
+                    }
+                }
+            } else {
+                // numpy random_poisson_mult, one uniform per iteration, lanes independent
+                int64_t X = 0;
+                double prod = 1.0;
+                for (int j = 0; j < nd;) {
+                    prod *= st.g.next_double();
+                    if (prod > c.enlam) {
+                        X += 1;
+                    } else {
+                        db[j * WAVE] = X;
+                        j++;
+                        X = 0;
+                        prod = 1.0;
+                    }
+                }
+            }
+#endif
+            double *pb = pbuf + cb * NP * WAVE + lane;
+            if (rs && mine) {                      // reset() of the owner: 5 uniforms (:105-111)
                 nv_reset_regs<LT>(P, e, st, nullptr, false);
 #pragma unroll
-                for (int j = 0; j < 5; j++) pbuf[(cb * 5 + j) * WAVE + lane] = st.par[j];
+                for (int j = 0; j < 5; j++) pb[j * WAVE] = st.par[j];
+                pb[5 * WAVE] = __longlong_as_double((long long)st.g.hi);
+                pb[6 * WAVE] = __longlong_as_double((long long)st.g.lo);
+            }
+            nv_wg_sync();   // barrier: chunk ready
+            if (rs) {                              // the new episode's branch owns the generator
+#pragma unroll
+                for (int j = 0; j < 5; j++) st.par[j] = pb[j * WAVE];
+                st.g.hi = (uint64_t)__double_as_longlong(pb[5 * WAVE]);
+                st.g.lo = (uint64_t)__double_as_longlong(pb[6 * WAVE]);
                 c = nv_rate_const(st.par[4]);
+                mine = nv_mult_branch(c.lam) == multw;
                 reset_any = true;
                 t = 0;
             } else {
-#ifdef INVSIM_ABL_ROLL_NO_DRAW
-                dbuf[(cb * CH + kk) * WAVE + lane] = 20;
-#else
-                dbuf[(cb * CH + kk) * WAVE + lane] = nv_poisson_c(st.g, c, lg_l);   // :146
-#endif
-                t++;
+                t += len;
             }
-            if (++kk == CH || rs || k == K - 1) {  // chunk closes
-                nv_wg_sync();
-                kk = 0;
-                cb ^= 1;
-            }
+            k0 += len;
+            cb ^= 1;
         }
         if (valid) {
-            P.cm.rng.store_state(e, st.g);
-            if (reset_any) {
+            if (mine) P.cm.rng.store_state(e, st.g);
+            if (reset_any && !multw) {
 #pragma unroll
                 for (int j = 0; j < 5; j++) P.par[j * S + e] = st.par[j];
             }
@@ -756,7 +836,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
         const bool rs = nxt && sc >= P.step_limit;
         if (rs) {                                                  // NEXT_STEP autoreset
 #pragma unroll
-            for (int j = 0; j < 5; j++) st.par[j] = pbuf[(cb * 5 + j) * WAVE + lane];
+            for (int j = 0; j < 5; j++) st.par[j] = pbuf[(cb * NP + j) * WAVE + lane];
 #pragma unroll
             for (int p = 0; p < LT; p++) st.pv[p] = 0.f;
             obs_params(st.par, trow);
@@ -894,7 +974,7 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
         if (ce != hipSuccess) return ce;
     }
     if (!pol && io.K > 1 && t_u >= 0 && p.L > 0 && p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
-        const dim3 gr(grid_for(p.cm.N, WAVE)), br(2 * WAVE);
+        const dim3 gr(grid_for(p.cm.N, WAVE)), br(3 * WAVE);
         bool done = true;
 #define R_(X)                                                                                              \
     do {                                                                                                   \
