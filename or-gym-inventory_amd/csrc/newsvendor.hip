@@ -681,8 +681,11 @@ __device__ __forceinline__ void nv_chunk(int t, int rem, int step_limit, bool nx
 // fill buffer c & 1, barrier c, the dynamics wave consumes chunk c after
 // barrier c.  Same draws, same order, same arithmetic as nv_run_kernel.
 template <int LT>
+#ifndef NV_ROLL_CH
+#define NV_ROLL_CH 8
+#endif
 struct NvRoll {
-    static constexpr int CH = 8;
+    static constexpr int CH = NV_ROLL_CH;
     static constexpr int O = LT + 5;
     static constexpr int NP = 7;   // reset handoff: price, cost, h, k, mu, state hi, state lo
     static constexpr size_t tile_bytes() { return (size_t)((EPW * O + 3) / 4) * 4 * sizeof(float); }
