@@ -582,6 +582,12 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
         // (INVSIM_NET_GENERIC=1 forces the generic one, for cross-checks)
         const char *gen = std::getenv("INVSIM_NET_GENERIC");
         h->net_spec = (gen && gen[0] == '1') ? NET_SPEC_NONE : net_spec_match(*s);
+        p.ahead = nullptr;
+        if (rc == INVSIM_OK && h->net_spec != NET_SPEC_NONE) {   // lookahead cache: 2 slots x (2 + RL) rows
+            hipError_t e = hipMalloc(&h->scratch, (size_t)(2 * (2 + p.RL) * h->Npad * sizeof(uint64_t)));
+            if (e != hipSuccess) rc = fail(h, INVSIM_ENOMEM, "hipMalloc(lookahead cache)");
+            else p.ahead = static_cast<uint64_t *>(h->scratch);
+        }
     }
     return finish_create(h, out, rc);
 }
@@ -644,6 +650,7 @@ static int commit_rng(invsim_handle *h, hipStream_t s) {
     hipError_t e = hipSuccess;
     if (h->family == INVSIM_INVMGMT) e = im_commit_launch(h->im, h->la_slot, s);
     else if (h->family == INVSIM_NEWSVENDOR) e = nv_commit_launch(h->nv, h->la_slot, s);
+    else if (h->family == INVSIM_NETINVMGMT) e = net_commit_launch(h->net, h->la_slot, s);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "rng commit");
 }
 
@@ -738,7 +745,8 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         case INVSIM_NETINVMGMT: {
             StepIO<float, float> io{K, (const float *)actions, (float *)obs, reward, terminated, truncated, (float *)final_obs};
             if (pol && !h->net_spec) return fail(h, INVSIM_EINVAL, "policy rollouts need the default or custom graph");
-            e = h->net_spec ? net_spec_launch(h->net_spec, h->net, t_u, pol, io, s) : net_run_launch(h->net, t_u, io, s);
+            e = h->net_spec ? net_spec_launch(h->net_spec, h->net, t_u, pol, io, h->la_valid, h->la_slot, s)
+                            : net_run_launch(h->net, t_u, io, s);
             break;
         }
         default: return fail(h, INVSIM_EINVAL, "bad handle family");

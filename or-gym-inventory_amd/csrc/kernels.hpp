@@ -119,6 +119,9 @@ struct NetParams {
     double *U;                   // [RL][Npad]
     double *Y;                   // [E][Npad]
     double *Rring;               // [sumL][Npad]
+    // demand lookahead cache of the specialised kernels (not part of the state
+    // blob): two slots of rows [state hi, state lo, demand per retail link] x Npad
+    uint64_t *ahead;
 };
 
 // Step I/O of one launch: K consecutive steps (K = 1 for invsim_step); row k
@@ -302,7 +305,8 @@ hipError_t im_commit_launch(const ImParams &p, int slot, hipStream_t s);
 // (netspec.hip): which built-in topology a spec equals, and its launcher.
 enum { NET_SPEC_NONE = 0, NET_SPEC_DEFAULT = 1, NET_SPEC_CUSTOM = 2 };
 hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const PolicyIO *pol,
-                           const StepIO<float, float> &io, hipStream_t s);
+                           const StepIO<float, float> &io, bool &ahead, int &slot, hipStream_t s);
+hipError_t net_commit_launch(const NetParams &p, int slot, hipStream_t s);
 hipError_t net_reset_launch(const NetParams &p, const uint8_t *mask, float *obs, hipStream_t s);
 hipError_t net_run_launch(const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s);
 size_t net_lds_bytes(const NetParams &p);

@@ -425,6 +425,169 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     (void)t_start;
 }
 
+// Single lock-step step (invsim_step: K = 1, t < T, no policy, no SAME_STEP
+// reset in this step) with the demand lookahead.  The market demands of a step
+// are Poisson draws of the env's own stream at fixed rates, and reset() draws
+// nothing (:301-332), so every launch can already draw the NEXT step's demands.
+// P.ahead: two slots of rows [state hi, state lo, demand per retail link] x
+// Npad, alternating per launch.
+//   HIT (slot cur holds each env's state RL draws past the committed one, and
+//        those draws): the step workgroups load the demands; `gla` workgroups
+//        at the front of the grid draw the next demands from slot cur's state
+//        into slot cur ^ 1, so the Poisson chain runs beside the step.
+//   !HIT: the step draws inline from cm.rng, leaves the state in slot cur, then
+//        draws the lookahead into slot cur ^ 1.
+// After the launch the committed state is slot cur; the host flips the slots,
+// and cm.rng is brought up to date from it (net_commit_kernel) only before
+// something reads it.  Streams are consumed in the reference's order;
+// arithmetic as net_spec_kernel.
+template <class G, bool HIT>
+__global__ void __launch_bounds__(WAVE)
+net_step1_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) {
+    extern __shared__ __attribute__((aligned(16))) float ns_lds[];
+    constexpr int O = G::O, RL = G::RL, NR = 2 + G::RL;
+    constexpr int TILE_IT = (EPW * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
+    constexpr int NT = RHS_LDS_MAX / WAVE;
+    const int lane = threadIdx.x;
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    const uint64_t *Acur = P.ahead + (int64_t)cur * NR * S;
+    uint64_t *Anxt = P.ahead + (int64_t)(cur ^ 1) * NR * S;
+    double *rhs_l = reinterpret_cast<double *>(ns_lds + ((EPW * O + 3) / 4) * 4);
+    PtrsConst pc[RL];
+#pragma unroll
+    for (int r = 0; r < RL; r++) pc[r] = P.rl_pc[r];
+    auto stage = [&](double (&tv)[RL][NT]) {
+#pragma unroll
+        for (int r = 0; r < RL; r++) {
+            const int qm = pc[r].nk > 0 ? pc[r].nk - 1 : 0;
+            const double *src = pc[r].nk > 0 ? P.rhs + pc[r].toff : P.alpha_pow;   // any valid pointer
+#pragma unroll
+            for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
+        }
+    };
+    auto flush = [&](const double (&tv)[RL][NT]) {
+#pragma unroll
+        for (int r = 0; r < RL; r++)
+#pragma unroll
+            for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
+        wave_lds_sync();
+    };
+    const int bid = (int)blockIdx.x;
+    if (HIT && bid < gla) {   // ---- lookahead workgroup: 64 envs, one per lane
+        const int64_t e = (int64_t)bid * WAVE + lane;
+        const bool valid = e < N;
+        const int64_t el = valid ? e : N - 1;
+        double tv[RL][NT];
+        stage(tv);
+        Pcg g;
+        g.hi = Acur[el];
+        g.lo = Acur[S + el];
+        g.inc_hi = P.cm.rng.inc_hi[el];
+        g.inc_lo = P.cm.rng.inc_lo[el];
+        flush(tv);
+        double Dd[RL];
+        spec_demand<G>(g, pc, rhs_l, Dd);
+        if (valid) {
+            st_store(Anxt + e, g.hi);
+            st_store(Anxt + S + e, g.lo);
+#pragma unroll
+            for (int r = 0; r < RL; r++) st_store(Anxt + (2 + r) * S + e, (uint64_t)(int64_t)Dd[r]);
+        }
+        return;
+    }
+    const int64_t e0 = (int64_t)(bid - (HIT ? gla : 0)) * EPW;
+    const int64_t e = e0 + lane;
+    const bool valid = e < N;
+    const int nvalid = (int)((N - e0) < EPW ? (N - e0) : EPW);
+    const int64_t el = valid ? e : N - 1;      // lanes past N mirror env N-1 (loads only)
+    float *tile = ns_lds;
+    float *trow = tile + lane * O;
+    NetSt<G> st;
+    double Dd[RL];
+    double tv[RL][NT];
+    if (HIT) {
+#pragma unroll
+        for (int r = 0; r < RL; r++) Dd[r] = (double)(int64_t)Acur[(2 + r) * S + el];
+    } else {
+        stage(tv);
+        st.g = P.cm.rng.load(el);
+    }
+    const double apow = P.alpha_pow[t];
+#pragma unroll
+    for (int j = 0; j < G::J; j++) st.X[j] = P.X[j * S + el];
+#pragma unroll
+    for (int r = 0; r < RL; r++) st.U[r] = P.U[r * S + el];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) st.Y[k] = P.Y[k * S + el];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {
+        if (G::L[k] == 0) continue;
+#pragma unroll
+        for (int a = 1; a <= G::L[k]; a++) {
+            const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+            const double v = P.Rring[(int64_t)row * S + el];
+            st.w[G::ring_off[k] + a - 1] = (t - a >= 0) ? v : 0.0;   // zeroed history (:315-321)
+        }
+    }
+    float act[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) act[k] = io.act[el * G::E + k];
+    if (!HIT) {
+        flush(tv);
+        spec_demand<G>(st.g, pc, rhs_l, Dd);                   // :536-541
+    }
+    double Rn[G::E];
+    double *irec = (valid && P.cm.info_rec) ? (double *)P.cm.info_rec + e * (2 * RL + 2 * G::J + 2 * G::E) : nullptr;
+    const double r = spec_dyn<G>(P, t, apow, st, act, Dd, trow, Rn, nullptr, irec);
+    if (valid) {
+        out_store(io.rew + e, r);
+        out_store(io.term + e, (uint8_t)0);
+        out_store(io.trunc + e, (uint8_t)(t + 1 >= P.T ? 1 : 0));
+        if (P.cm.info_demand) {
+#pragma unroll
+            for (int q = 0; q < RL; q++) P.cm.info_demand[e * RL + q] = (int64_t)Dd[q];
+        }
+    }
+    wave_lds_sync();
+    store_tile<TILE_IT>(tile, io.obs + e0 * O, (int64_t)nvalid * O, lane);
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < G::E; k++)
+            if (G::L[k] > 0)
+                st_store(P.Rring + (int64_t)(G::ring_off[k] + (int)((uint32_t)t % (uint32_t)G::L[k])) * S + e, Rn[k]);
+#pragma unroll
+        for (int j = 0; j < G::J; j++) st_store(P.X + j * S + e, st.X[j]);
+#pragma unroll
+        for (int q = 0; q < RL; q++) st_store(P.U + q * S + e, st.U[q]);
+#pragma unroll
+        for (int k = 0; k < G::E; k++) st_store(P.Y + k * S + e, st.Y[k]);
+    }
+    if (!HIT) {   // committed state (after this step's draws) -> slot cur; the lookahead -> slot cur ^ 1
+        if (valid) {
+            st_store((uint64_t *)Acur + e, st.g.hi);
+            st_store((uint64_t *)Acur + S + e, st.g.lo);
+        }
+        spec_demand<G>(st.g, pc, rhs_l, Dd);
+        if (valid) {
+            st_store(Anxt + e, st.g.hi);
+            st_store(Anxt + S + e, st.g.lo);
+#pragma unroll
+            for (int q = 0; q < RL; q++) st_store(Anxt + (2 + q) * S + e, (uint64_t)(int64_t)Dd[q]);
+        }
+    }
+}
+
+// cm.rng <- the committed slot of the lookahead cache
+__global__ void __launch_bounds__(256) net_commit_kernel(NetParams P, int slot, int nr) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P.cm.N) return;
+    const int64_t S = P.cm.Npad;
+    const uint64_t *A = P.ahead + (int64_t)slot * nr * S;
+    P.cm.rng.hi[e] = A[e];
+    P.cm.rng.lo[e] = A[S + e];
+}
+
 // Cross-wave LDS handoff inside a workgroup: orders LDS traffic only (an
 // __syncthreads() would also drain each wave's outstanding global loads and
 // stores, s_waitcnt vmcnt(0), before the s_barrier)
@@ -665,13 +828,37 @@ static size_t spec_lds_bytes() {
     return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float) + (size_t)G::RL * RHS_LDS_MAX * sizeof(double);
 }
 
+// INVSIM_NET_AHEAD=0 turns the step's demand lookahead off (A/B measurements)
+static bool net_ahead_enabled() {
+    const char *v = getenv("INVSIM_NET_AHEAD");
+    return !(v && v[0] == '0');
+}
+
 template <class G>
 static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
-                              hipStream_t s) {
+                              bool &ahead, int &slot, hipStream_t s) {
     const size_t lds = spec_lds_bytes<G>();
     const dim3 grid((unsigned)((p.cm.N + EPW - 1) / EPW)), block(WAVE);
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
+    if (p.ahead && net_ahead_enabled() && !pol && io.K == 1 && t_u >= 0 && t_u < p.T && io.obs &&
+        !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.T)) {
+        const bool hit = ahead;
+        const int gla = hit ? (int)((p.cm.N + WAVE - 1) / WAVE) : 0;
+        const dim3 grid2(grid.x + gla);
+        if (hit) hipLaunchKernelGGL((net_step1_kernel<G, true>), grid2, block, lds, s, p, t_u, io, slot, gla);
+        else hipLaunchKernelGGL((net_step1_kernel<G, false>), grid2, block, lds, s, p, t_u, io, slot, gla);
+        ahead = true;
+        slot ^= 1;
+        return hipGetLastError();
+    }
+    // the other kernels draw from cm.rng: commit the cache first (the lock-step
+    // NEXT_STEP autoreset launch draws nothing and keeps it)
+    if (ahead && !(!pol && io.K == 1 && t_u >= p.T)) {
+        const hipError_t ce = net_commit_launch(p, slot, s);
+        ahead = false;
+        if (ce != hipSuccess) return ce;
+    }
 #define K_(TU, ONE, POL) hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
     if (!pol && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
         (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
@@ -693,12 +880,19 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
     return hipGetLastError();
 }
 
+hipError_t net_commit_launch(const NetParams &p, int slot, hipStream_t s) {
+    if (p.cm.N == 0 || !p.ahead) return hipSuccess;
+    hipLaunchKernelGGL(net_commit_kernel, dim3((unsigned)((p.cm.N + 255) / 256)), dim3(256), 0, s, p, slot ^ 1,
+                       2 + p.RL);
+    return hipGetLastError();
+}
+
 hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const PolicyIO *pol,
-                           const StepIO<float, float> &io, hipStream_t s) {
+                           const StepIO<float, float> &io, bool &ahead, int &slot, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     switch (which) {
-        case NET_SPEC_DEFAULT: return spec_launch<NetTopoDefault>(p, t_u, pol, io, s);
-        case NET_SPEC_CUSTOM: return spec_launch<NetTopoCustom>(p, t_u, pol, io, s);
+        case NET_SPEC_DEFAULT: return spec_launch<NetTopoDefault>(p, t_u, pol, io, ahead, slot, s);
+        case NET_SPEC_CUSTOM: return spec_launch<NetTopoCustom>(p, t_u, pol, io, ahead, slot, s);
         default: return hipErrorInvalidValue;
     }
 }

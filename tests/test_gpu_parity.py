@@ -769,3 +769,84 @@ def test_newsvendor_stream_wave_rollout_equals_one_wave(gpu, monkeypatch, L, ste
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
     monkeypatch.delenv("INVSIM_NV_ROLL")
+
+
+@pytest.mark.parametrize("graph,kw", [("default", dict(autoreset_mode="next_step")),
+                                      ("default", dict(autoreset_mode="disabled")),
+                                      ("default", dict(autoreset_mode="same_step")),
+                                      ("custom", dict(autoreset_mode="next_step", backlog=False))])
+def test_net_demand_lookahead_mixed_calls(gpu, graph, kw, monkeypatch):
+    """Compiled-network steps draw the NEXT step's market demands into a
+    lookahead cache (net_step1_kernel) while the committed generator state
+    stays exact.  Steps, rollouts, policy rollouts, seeds, checkpoints, masked
+    and explicit resets and episode boundaries give the same outputs, demands,
+    step records and state blobs as a cache-free run (INVSIM_NET_AHEAD=0)."""
+    import invsim
+    from invsim.policies import ConstantOrderAgent
+    from invsim.topology import custom_graph, default_graph
+    mk_g = default_graph if graph == "default" else custom_graph
+    n = 777
+    envs = [invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), num_periods=9, record_demand=True,
+                                       record_info=True, **kw) for _ in range(2)]
+    A_dim = envs[0].action_dim
+    g = torch.Generator(device=gpu).manual_seed(5)
+    A = torch.rand((200, n, A_dim), device=gpu, generator=g) * 200 - 5
+    pos = [0]
+
+    def both(fn):
+        outs = []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_NET_AHEAD", "1" if i == 0 else "0")
+            outs.append(fn(env))
+        return outs
+
+    def steps(k):
+        for _ in range(k):
+            a = A[pos[0] % 200]
+            pos[0] += 1
+
+            def one(env):
+                o, r, te, tr, info = env.step(a)
+                out = [o.clone(), r.clone(), te.clone(), tr.clone(), env._demand.clone()]
+                if "final_obs" in info:
+                    out.append(info["final_obs"][tr].clone())
+                return out
+            o = both(one)
+            for x, y in zip(o[0], o[1]):
+                assert torch.equal(x, y), pos[0]
+
+    def same_state():
+        s = both(lambda env: env.get_state().clone())
+        assert torch.equal(s[0], s[1]), pos[0]
+
+    both(lambda env: env.reset(seed=21))
+    steps(5)
+    same_state()
+    if kw["autoreset_mode"] == "same_step":
+        steps(7)                                             # crosses the horizon (reset in the done step)
+    elif kw["autoreset_mode"] != "disabled":
+        o = both(lambda env: env.rollout(A[:3]))             # other kernels after a lookahead
+        assert all(torch.equal(x, y) for x, y in zip(o[0], o[1]))
+        steps(4)                                             # crosses the horizon
+    else:
+        steps(4)
+        both(lambda env: env.reset())
+    ck = both(lambda env: env.get_state().clone())
+    steps(3)
+    both(lambda env: env.reset(seed=22))                    # re-seed invalidates the cache
+    steps(2)
+    both(lambda env: env.set_state(ck[0].clone()))          # back to the checkpoint
+    steps(1)
+    both(lambda env: env.reset())
+    steps(4)
+    if kw["autoreset_mode"] != "same_step":
+        m = both(lambda env: env.rollout_policy(ConstantOrderAgent(0.3), 2, obs=True))
+        assert all(torch.equal(m[0][k], m[1][k]) for k in m[0])
+    steps(3 if kw["autoreset_mode"] != "disabled" else 1)  # disabled: no env may pass the horizon
+    mask = torch.zeros(n, dtype=torch.bool, device=gpu)
+    mask[::5] = True
+    both(lambda env: env.reset(options={"reset_mask": mask}))
+    steps(3 if kw["autoreset_mode"] != "disabled" else 1)
+    both(lambda env: env.reset())
+    steps(12 if kw["autoreset_mode"] != "disabled" else 8)
+    same_state()
