@@ -1132,6 +1132,315 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
     }
 }
 
+// im_roll3_kernel with the observation work moved to a third wave (for small
+// batches, where a dynamics wave has a SIMD to itself and its instruction
+// chain is the step time): one 192-thread workgroup per 64 envs, three roles
+// pipelined over chunks of CH launch steps:
+//   wave 0 (demand)   draws the demands of chunk c + 1 into a double-buffered
+//                     LDS ring; a demand is a function of the env's stream only,
+//                     and a NEXT_STEP reset step draws nothing (:186-222)
+//   wave 1 (dynamics) consumes chunk c: the step (:224-352) with the
+//                     fulfilled-order history in registers aligned by age
+//                     (rw_i[a] = R[t - L_i + a], so the arrival is rw_i[0]);
+//                     stores reward, flags, the new R ring slots, and hands the
+//                     end-of-step inventory of every step to wave 2 in LDS
+//   wave 2 (obs)      builds the observations of chunk c - 1: the inventory
+//                     from wave 1, the requested-order rows from its own copy
+//                     of the actions (wv[a] = action_log[t - (D - 1) + a], in
+//                     registers), the obs tile store, and the action_log ring
+// Each role's next step's actions / alpha**t are loaded a step ahead, before
+// the previous step's stores (vmcnt is in order).  One barrier per chunk: the
+// demand wave fills dbuf[c & 1] before barrier c, the dynamics wave consumes it
+// between barriers c and c + 1 and fills ibuf[c & 1], which the obs wave
+// consumes between barriers c + 1 and c + 2.  Same arithmetic, in the same
+// order, as im_step_regs.
+template <int L0, int L1, int L2>
+struct ImLt3o : ImLt3<L0, L1, L2> {
+    static constexpr int CH = 4;                                         // chunk (launch steps)
+    static constexpr int M1 = 3, O = ImLt3<L0, L1, L2>::O;
+    static constexpr size_t lds() {
+        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + 2 * CH * WAVE * 8 + 2 * CH * M1 * WAVE * 8;
+    }
+};
+
+template <int L0, int L1, int L2, bool BACKLOG>
+__global__ void __launch_bounds__(3 * WAVE)
+im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
+    using G = ImLt3o<L0, L1, L2>;
+    constexpr int M1 = G::M1, D = G::D, O = G::O, CH = G::CH;
+    extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
+    double *rhs_l = reinterpret_cast<double *>(im_tile + WAVE * O);
+    int64_t *dbuf = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);   // [2][CH][WAVE]
+    int64_t *ibuf = dbuf + 2 * CH * WAVE;                                 // [2][CH][M1][WAVE]
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int role = threadIdx.x / WAVE;
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e = e0 + lane;
+    const bool valid = e < N;
+    const int64_t el = valid ? e : N - 1;          // padded lanes: the last env's data, never stored
+    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
+    const int K = io.K;
+    const int nch = (K + CH - 1) / CH;
+    if (role == 0) {   // ---- demand wave
+        TableStage ts;
+        ts.dst = rhs_l;
+        {
+            const bool has_tab = P.pc.nk > 0;
+            const double *tsrc = has_tab ? P.rhs : P.alpha_pow;   // any valid pointer
+            const int qm = has_tab ? P.pc.nk - 1 : 0;
+#pragma unroll
+            for (int u = 0; u < TableStage::NT; u++) ts.v[u] = tsrc[min(lane + u * WAVE, qm)];
+        }
+        Pcg g = P.cm.rng.load(el);
+        ts.flush(lane);
+        int t = t_start;
+        for (int c = 0; c < nch; c++) {
+            int64_t *db = dbuf + (c & 1) * CH * WAVE;
+            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+                if (t >= P.periods) {              // NEXT_STEP reset step: no draw
+                    t = 0;
+                    continue;
+                }
+#ifdef INVSIM_ABL_ROLL_NO_DRAW
+                int64_t d = 20;
+#else
+                int64_t d = env_poisson(g, P.pc, rhs_l);                // :280
+#endif
+                db[kk * WAVE + lane] = d < 0 ? 0 : d;
+                t++;
+            }
+            wg_lds_sync();   // barrier c: demand chunk c ready
+        }
+        wg_lds_sync();       // barrier nch: the obs wave's last chunk
+        if (valid) P.cm.rng.store_state(e, g);
+        return;
+    }
+    if (role == 2) {   // ---- obs wave
+        int64_t *trow = im_tile + (int64_t)lane * O;
+        int t = t_start;
+        // requested-order rows: wv[a] = action_log[t - (D - 1) + a], slot (t + 1 + a) mod D
+        int64_t wv[D > 1 ? D - 1 : 1][M1];
+#pragma unroll
+        for (int a = 0; a + 1 < D; a++) {
+            const int64_t base = ((int64_t)((uint32_t)(t + 1 + a) % (uint32_t)D) * S + el) * M1;
+#pragma unroll
+            for (int i = 0; i < M1; i++) {
+                const uint32_t v = P.alog32[base + i];
+                wv[a][i] = (int64_t)v;
+                if (v == IM_WIDE) wv[a][i] = P.alog[base + i];
+            }
+        }
+        int64_t nact[M1];
+#pragma unroll
+        for (int i = 0; i < M1; i++) nact[i] = io.act[el * M1 + i];
+        wg_lds_sync();   // barrier 0
+        for (int c = 0; c < nch; c++) {
+            wg_lds_sync();   // barrier c + 1: inventory chunk c ready
+            const int64_t *ib = ibuf + (c & 1) * CH * M1 * WAVE;
+            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+                const int k = c * CH + kk;
+                int64_t req[M1];
+#pragma unroll
+                for (int i = 0; i < M1; i++) req[i] = nact[i];
+                if (k + 1 < K) {                       // the next step's actions
+#pragma unroll
+                    for (int i = 0; i < M1; i++) nact[i] = io.act[((int64_t)(k + 1) * N + el) * M1 + i];
+                }
+                if (t >= P.periods) {                  // NEXT_STEP autoreset: [I0, 0...] (:220)
+#pragma unroll
+                    for (int q = 0; q < O; q++) trow[q] = (q < M1) ? ib[(kk * M1 + q) * WAVE + lane] : 0;
+                    t = 0;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < M1; i++) req[i] = req[i] > 0 ? req[i] : 0;   // :250
+                    // observation (:354-391): I, then the window rows t+1-n .. t, zeros after
+                    const int n = (t + 1 < D) ? t + 1 : D;
+#pragma unroll
+                    for (int i = 0; i < M1; i++) trow[i] = ib[(kk * M1 + i) * WAVE + lane];
+#pragma unroll
+                    for (int a = 0; a + 1 < D; a++) {
+                        const int r = a - D + n;                                // obs row of wv[a]
+                        if (r >= 0) {
+#pragma unroll
+                            for (int i = 0; i < M1; i++) trow[M1 + r * M1 + i] = wv[a][i];
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < M1; i++) trow[M1 + (n - 1) * M1 + i] = req[i];
+                    for (int q = M1 + n * M1; q < O; q++) trow[q] = 0;
+                    if (valid) {                                                // action_log[t] (:268)
+                        const int64_t wb = ((int64_t)((uint32_t)t % (uint32_t)D) * S + e) * M1;
+#pragma unroll
+                        for (int i = 0; i < M1; i++) {
+                            const bool wide = req[i] >= (int64_t)IM_WIDE;
+                            st_store(P.alog32 + wb + i, wide ? IM_WIDE : (uint32_t)req[i]);
+                            if (wide) st_store(P.alog + wb + i, req[i]);
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a + 2 < D; a++) {
+#pragma unroll
+                        for (int i = 0; i < M1; i++) wv[a][i] = wv[a + 1][i];
+                    }
+                    if (D > 1) {
+#pragma unroll
+                        for (int i = 0; i < M1; i++) wv[D - 2][i] = req[i];
+                    }
+                    t += 1;
+                }
+                wave_lds_sync();
+#ifndef INVSIM_ABL_ROLL_NO_STORE
+                store_tile<(O * WAVE * 8 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + ((int64_t)k * N + e0) * O,
+                                                                        (int64_t)nvalid * O, lane);
+#endif
+                wave_lds_sync();
+            }
+        }
+        return;
+    }
+    // ---- dynamics wave
+    int t = t_start;
+    int64_t I[M1], B[M1 + 1];
+#pragma unroll
+    for (int i = 0; i < M1; i++) I[i] = P.I[i * S + el];
+#pragma unroll
+    for (int q = 0; q <= M1; q++) B[q] = BACKLOG ? P.B[q * S + el] : 0;
+    // fulfilled-order windows: rw_i[a] = R[t - L_i + a] from ring slot (t + a) mod L_i
+    // (rows older than the episode are masked at use by t >= L_i)
+    int64_t rw[M1][D > 0 ? D : 1];                 // stage i uses rw[i][0 .. W(i))
+#pragma unroll
+    for (int i = 0; i < M1; i++) {
+#pragma unroll
+        for (int a = 0; a < G::W(i); a++) {
+            const int L = G::lt(i);
+            rw[i][a] = L > 0 ? P.Rring[(int64_t)(P.ring_off[i] + (int)((uint32_t)(t + a) % (uint32_t)L)) * S + el] : 0;
+        }
+    }
+    int64_t nact[M1];
+#pragma unroll
+    for (int i = 0; i < M1; i++) nact[i] = io.act[el * M1 + i];
+    double napow = P.alpha_pow[t < P.periods ? t : 0];   // alpha**t of the next step, prefetched
+    int64_t dlast = 0;
+    bool last_real = false;
+    wg_lds_sync();   // barrier 0: demand chunk 0 ready
+    for (int c = 0; c < nch; c++) {
+        const int64_t *db = dbuf + (c & 1) * CH * WAVE;
+        int64_t *ib = ibuf + (c & 1) * CH * M1 * WAVE;
+        for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+            const int k = c * CH + kk;
+            const int64_t oi = (int64_t)k * N + e;
+            int64_t req[M1];
+#pragma unroll
+            for (int i = 0; i < M1; i++) req[i] = nact[i];
+            const double apow = napow;
+            {
+                const int tn = (t >= P.periods) ? 0 : t + 1;     // the next launch step's period
+                napow = P.alpha_pow[tn < P.periods ? tn : 0];
+            }
+            if (k + 1 < K) {                       // prefetch the next step's actions
+#pragma unroll
+                for (int i = 0; i < M1; i++) nact[i] = io.act[((int64_t)(k + 1) * N + el) * M1 + i];
+            }
+            if (t >= P.periods) {                  // NEXT_STEP autoreset (:197-220)
+#pragma unroll
+                for (int i = 0; i < M1; i++) I[i] = P.I0[i];
+#pragma unroll
+                for (int q = 0; q <= M1; q++) B[q] = 0;
+#pragma unroll
+                for (int i = 0; i < M1; i++) ib[(kk * M1 + i) * WAVE + lane] = I[i];
+                if (valid) {
+                    out_store(io.rew + oi, 0.0);
+                    out_store(io.term + oi, (uint8_t)0);
+                    out_store(io.trunc + oi, (uint8_t)0);
+                }
+                t = 0;
+            } else {
+                const int64_t d = db[kk * WAVE + lane];
+                int64_t ordreq[M1], R[M1], Icur[M1];
+#pragma unroll
+                for (int i = 0; i < M1; i++) req[i] = req[i] > 0 ? req[i] : 0;   // :250
+#pragma unroll
+                for (int i = 0; i < M1; i++) {
+                    ordreq[i] = wrap_add(req[i], B[i + 1]);                     // :253-255
+                    const int64_t r = ordreq[i] < P.c[i] ? ordreq[i] : P.c[i];  // :263
+                    R[i] = (i + 1 < M1) ? min_via_f64(r, I[i + 1]) : (int64_t)(double)r;   // :260-265
+                }
+#pragma unroll
+                for (int i = 0; i < M1; i++) {                                  // arrivals (:271-277)
+                    const int L = G::lt(i);
+                    const int64_t arr = (L > 0 && t >= L) ? rw[i][0] : 0;
+                    Icur[i] = wrap_add(I[i], L == 0 ? R[i] : arr);
+                }
+#pragma unroll
+                for (int i = 1; i < M1; i++) Icur[i] = wrap_sub(Icur[i], R[i]); // :300 (reference quirk, kept)
+                int64_t Sv[M1 + 1], U[M1 + 1];
+#pragma unroll
+                for (int i = 0; i < M1; i++) {
+                    Sv[i + 1] = R[i];                                           // :295
+                    U[i + 1] = wrap_sub(ordreq[i], R[i]);                       // :304
+                }
+                const int64_t dfill = wrap_add(d, B[0]);                        // :284-286
+                const int64_t s0 = Icur[0] < dfill ? Icur[0] : dfill;           // :288
+                Icur[0] = wrap_sub(Icur[0], s0);
+                Sv[0] = s0;
+                U[0] = wrap_sub(dfill, s0);                                     // :303
+                double term[M1 + 1];                                            // :315-321
+#pragma unroll
+                for (int q = 0; q <= M1; q++) {
+                    const double Sj = (double)Sv[q];
+                    const int64_t inv = (q < M1) ? Icur[q] : 0;
+                    const double hold = P.hc[q] * (double)(inv > 0 ? inv : 0);
+                    term[q] = ((P.up[q] * Sj - P.uc[q] * Sj) - hold) - P.kc[q] * (double)U[q];
+                }
+                const double profit = np_sum<double>(M1 + 1, [&](int q) { return term[q]; });
+                const double reward = apow * profit;                            // :322
+#pragma unroll
+                for (int i = 0; i < M1; i++) ib[(kk * M1 + i) * WAVE + lane] = Icur[i];   // obs I (:366)
+                // the new fulfilled-order ring slots R[t] (:267)
+                if (valid) {
+#pragma unroll
+                    for (int i = 0; i < M1; i++) {
+                        const int L = G::lt(i);
+                        if (L > 0) st_store(P.Rring + (int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e, R[i]);
+                    }
+                    out_store(io.rew + oi, reward);
+                    out_store(io.term + oi, (uint8_t)0);
+                    out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.periods ? 1 : 0));   // :350
+                }
+                // age the windows by one period
+#pragma unroll
+                for (int i = 0; i < M1; i++) {
+                    const int L = G::lt(i);
+                    if (L > 0) {
+#pragma unroll
+                        for (int a = 0; a + 1 < G::W(i); a++) rw[i][a] = rw[i][a + 1];
+                        rw[i][G::W(i) - 1] = R[i];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < M1; i++) I[i] = Icur[i];                    // :326
+#pragma unroll
+                for (int q = 0; q <= M1; q++) B[q] = BACKLOG ? U[q] : 0;        // :307-312
+                dlast = d;
+                last_real = k == K - 1;
+                t += 1;
+            }
+        }
+        wg_lds_sync();   // barrier c + 1: inventory chunk c ready, demand chunk c + 1 ready
+    }
+    if (valid) {
+#pragma unroll
+        for (int i = 0; i < M1; i++) st_store(P.I + i * S + e, I[i]);
+        if (BACKLOG) {
+#pragma unroll
+            for (int q = 0; q <= M1; q++) st_store(P.B + q * S + e, B[q]);
+        }
+        if (P.cm.info_demand && last_real) P.cm.info_demand[e] = dlast;
+    }
+}
+
 // cm.rng <- the committed slot of the lookahead cache (see im_split_kernel)
 __global__ void __launch_bounds__(256) im_commit_kernel(ImParams P, int slot) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1158,6 +1467,12 @@ inline bool im_la_last() {
 }
 
 // INVSIM_IM_ROLL=0 keeps rollouts on the one-wave kernel (A/B measurements, tests)
+// largest batch for the 3-role rollout (INVSIM_IM_ROLL3O_MAX_N overrides: A/B, tests)
+inline int64_t im_roll3o_max_n() {
+    const char *v = getenv("INVSIM_IM_ROLL3O_MAX_N");
+    return v ? (int64_t)atoll(v) : 32768;
+}
+
 inline bool im_roll_enabled() {
     const char *s = getenv("INVSIM_IM_ROLL");
     return !(s && s[0] == '0');
@@ -1241,9 +1556,19 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     if (!pol && io.K > 1 && t_u >= 0 && p.cm.autoreset != AR_SAME_STEP && p.dist == 1 && !p.cm.info_rec &&
         M1 == 3 && p.L[0] == 1 && p.L[1] == 5 && p.L[2] == 10 && p.lt_max == 10 && im_roll_enabled()) {
         using G = ImLt3<1, 5, 10>;
-        const dim3 g3(grid_for(p.cm.N, WAVE)), b3(2 * WAVE);
-        if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true>), g3, b3, G::lds(), s, p, t_u, io);
-        else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false>), g3, b3, G::lds(), s, p, t_u, io);
+        using G3 = ImLt3o<1, 5, 10>;
+        const dim3 g3(grid_for(p.cm.N, WAVE));
+        // up to one 2-role workgroup per SIMD pair (N <= 32768): the dynamics
+        // wave's chain is the step time, so split it (measured on MI355X:
+        // LostSales 32768 envs 87.5 -> 77.7 us per K = 30; at 65536 the
+        // 2-role kernel is faster, 118 vs 152 us)
+        if (p.cm.N <= im_roll3o_max_n()) {
+            if (backlog) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, true>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io);
+            else hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, false>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io);
+        } else {
+            if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io);
+            else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io);
+        }
         return hipGetLastError();
     }
 #define K_(M, B, TU, ONE, POL)                                                                         \

@@ -850,3 +850,31 @@ def test_net_demand_lookahead_mixed_calls(gpu, graph, kw, monkeypatch):
     both(lambda env: env.reset())
     steps(12 if kw["autoreset_mode"] != "disabled" else 8)
     same_state()
+
+
+@pytest.mark.parametrize("cls,n", [("InvManagementBacklogEnv", 3000), ("InvManagementLostSalesEnv", 32768)])
+def test_invmgmt_three_role_rollout_equals_two_role(gpu, monkeypatch, cls, n):
+    """Small batches run im_roll3o_kernel (obs work on a third wave); forcing
+    INVSIM_IM_ROLL3O_MAX_N=0 keeps them on im_roll3_kernel.  Same state in:
+    identical outputs, demand record and state out."""
+    import invsim
+    envs = []
+    for i in range(2):
+        env = getattr(invsim, cls)(n, device=gpu, record_demand=True)
+        env.reset(seed=17)
+        envs.append(env)
+    g = torch.Generator(device=gpu).manual_seed(3)
+    for K in (75, 9, 2):
+        a = torch.randint(-5, 260, (K, n, 3), device=gpu, dtype=torch.int64, generator=g)
+        a[:, ::89, 2] = (1 << 33) + 1          # wide requested orders
+        outs, dems = [], []
+        for i, env in enumerate(envs):
+            if i == 1:
+                monkeypatch.setenv("INVSIM_IM_ROLL3O_MAX_N", "0")
+            outs.append(env.rollout(a))
+            dems.append(env._demand.clone())
+            monkeypatch.delenv("INVSIM_IM_ROLL3O_MAX_N", raising=False)
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), K
+        assert torch.equal(dems[0], dems[1])
+        assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
