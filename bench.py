@@ -12,7 +12,8 @@ Multi-GPU (one process per GPU, torchrun): each rank owns 65 536 envs with
 global seeds rank*65536+i (weak scaling), no collective in the data path;
 barrier + synchronize around the timed region, max time over ranks.  After
 the timed region the per-rank episodic-return statistics are all-reduced over
-RCCL (the only cross-GPU exchange the path has).
+RCCL (the only cross-GPU exchange the path has).  --strong splits the
+workload's env count over the ranks instead (strong scaling).
 
 Prints ONE JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per
 launch (SURVEY §8(d) B1 x N) / mean kernel time from HIP events on the stream
@@ -56,6 +57,8 @@ def parse():
     ap.add_argument("--mode", default="step", choices=["step", "rollout"])
     ap.add_argument("--rollout-k", type=int, default=30)
     ap.add_argument("--n-envs", type=int, default=0)
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: the workload's env count is the GLOBAL batch, split over ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--pool", type=int, default=16, help="distinct action batches cycled")
@@ -156,6 +159,8 @@ def main():
     import invsim
     wl = WORKLOADS[args.workload]
     n = args.n_envs or wl["n"]
+    if args.strong:
+        n = (n + world - 1) // world                      # this rank's share of the global batch
     env = getattr(invsim, wl["cls"])(n, device=dev, global_offset=rank * n, copy=False)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
@@ -258,7 +263,7 @@ def main():
         "warmup": warm * steps_per_call,
         "ms_per_step": el * 1e3 / total_steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": wl["dtype"],
         "data": "synthetic (pre-generated random actions in HBM, seeds 0..N-1 per global env index)",
