@@ -878,3 +878,59 @@ def test_invmgmt_three_role_rollout_equals_two_role(gpu, monkeypatch, cls, n):
             assert torch.equal(x, y), K
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
+
+
+@pytest.mark.parametrize("family,cls_name,n", [
+    ("im", "InvManagementBacklogEnv", 65536),       # im_roll3_kernel
+    ("im", "InvManagementLostSalesEnv", 32768),     # im_roll3o_kernel (per-GPU shard of 262 144)
+    ("net", "NetInvMgmtBacklogEnv", 32768),         # net_roll_kernel, then net_step1_kernel
+    ("nv", "NewsvendorEnv", 65536),                 # nv_roll_kernel
+])
+def test_full_size_rollout_vs_oracle(gpu, oracle, family, cls_name, n):
+    """BASELINE-size fused rollouts across episode boundaries (NEXT_STEP resets
+    inside the launch), then single steps, checked step by step against the C
+    oracle stepping the same seeds: bit-exact obs, rewards and flags."""
+    import invsim
+    oracle.set_threads(8)
+    try:
+        env = getattr(invsim, cls_name)(n, device=gpu)
+        rng = np.random.default_rng(11)
+        if family == "im":
+            orc = oracle.OracleInvMgmt(n, backlog=cls_name.endswith("BacklogEnv"))
+            T, K = 30, 61
+            acts = np.stack([_im_random_actions(rng, n, 3, [100, 200, 230]) for _ in range(K + 3)])
+        elif family == "net":
+            orc = oracle.OracleNet(n)
+            T, K = 30, 61
+            acts = rng.uniform(-5, 300, size=(K + 3, n, 11)).astype(np.float32)
+        else:
+            orc = oracle.OracleNewsvendor(n)
+            T, K = 40, 81
+            acts = rng.uniform(-50, 2500, size=(K + 3, n, 1)).astype(np.float32)
+        orc.seed(range(300, 300 + n))
+        e_obs = orc.reset()
+        obs, _ = env.reset(seed=300)
+        assert _eq_bits(obs.cpu().numpy(), e_obs)
+        dev_acts = torch.from_numpy(acts).to(gpu)
+        o, r, te, tr = env.rollout(dev_acts[:K])
+        o, r, tr = o.cpu().numpy(), r.cpu().numpy(), tr.cpu().numpy()
+        t = 0
+        for k in range(K + 3):
+            if k < K:
+                go, gr, gt = o[k], r[k], tr[k]
+            else:                                   # single steps after the rollout
+                so, sr, _, st, _ = env.step(dev_acts[k])
+                go, gr, gt = so.cpu().numpy(), sr.cpu().numpy(), st.cpu().numpy()
+            if t >= T:                              # NEXT_STEP autoreset step
+                e_obs = orc.reset()
+                assert _eq_bits(go, e_obs), k
+                assert (gr == 0).all() and not gt.any(), k
+                t = 0
+                continue
+            res = orc.step(acts[k])
+            assert _eq_bits(go, res[0]), f"obs step {k}"
+            _assert_reward(gr, res[1], f"step {k}")
+            assert np.array_equal(gt, res[2]), k
+            t += 1
+    finally:
+        oracle.set_threads(1)
