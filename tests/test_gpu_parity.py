@@ -934,3 +934,31 @@ def test_full_size_rollout_vs_oracle(gpu, oracle, family, cls_name, n):
             t += 1
     finally:
         oracle.set_threads(1)
+
+
+@pytest.mark.parametrize("mu_max,step_limit", [(9.0, 40), (14.0, 6), (60.0, 40), (200.0, 5)])
+def test_newsvendor_rollout_sampler_mixes(gpu, monkeypatch, mu_max, step_limit):
+    """nv_roll_kernel's two stream waves (PTRS / multiplication branch) under
+    every mix of rates -- all envs on the multiplication method, mixed, all
+    PTRS -- and episodes shorter than a chunk give nv_run_kernel's outputs,
+    demands and state."""
+    import invsim
+    n = 3000
+    envs = []
+    for i in range(2):
+        env = invsim.NewsvendorEnv(n, device=gpu, mu_max=mu_max, step_limit=step_limit, record_demand=True)
+        env.reset(seed=77)
+        envs.append(env)
+    g = torch.Generator(device=gpu).manual_seed(2)
+    for K in (45, 8):
+        a = torch.rand((K, n, 1), device=gpu, generator=g) * 300
+        outs, dems = [], []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_NV_ROLL", "1" if i == 0 else "0")
+            outs.append(env.rollout(a))
+            dems.append(env._demand.clone())
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), K
+        assert torch.equal(dems[0], dems[1])
+        assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
+    monkeypatch.delenv("INVSIM_NV_ROLL")
