@@ -755,8 +755,24 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         h->la_valid = false;
         return hip_fail(h, e, "step launch");
     }
-    if (h->t_known)
+    if (h->t_known) {
         for (int k = 0; k < K; k++) h->t_cur = next_period(h->t_cur, h->horizon, h->cm.autoreset, h->past_ok);
+    } else if (h->cm.autoreset == AR_DISABLED && !h->past_ok) {
+        // per-env periods (after a masked reset): the kernels skip an env stepped
+        // past its horizon and flag it; surface that now, as the reference's
+        // IndexError (inventory_management.py:267), at the cost of one sync
+        uint32_t flags = 0;
+        e = hipMemcpyAsync(&flags, h->cm.status, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(h, e, "status read");
+        if (flags & 1u) {
+            e = hipMemsetAsync(h->cm.status, 0, sizeof(uint32_t), s);
+            if (e != hipSuccess) return hip_fail(h, e, "status clear");
+            return fail(h, INVSIM_ERANGE,
+                        "an env was stepped past its episode horizon with autoreset disabled (that env's step was "
+                        "not applied; its outputs are undefined); reset it first");
+        }
+    }
     return INVSIM_OK;
 }
 

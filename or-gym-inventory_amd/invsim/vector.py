@@ -259,7 +259,8 @@ class InvSimVectorEnv:
 
     def status(self, clear=True):
         """Sticky device status word (synchronous): bit 0 = an env was stepped past its
-        horizon with autoreset disabled after a masked reset (the step was not applied)."""
+        horizon with autoreset disabled after a masked reset (the step was not applied).
+        step()/rollout() already check it in that mode and raise IndexError."""
         f = _capi.C.c_uint32()
         _capi.check(self._lib.invsim_status(self._h, _capi.C.byref(f), int(clear)), self._h, "status")
         return f.value

@@ -339,6 +339,30 @@ def test_disabled_mode_horizon_raises(gpu):
         env.step(a)
 
 
+@pytest.mark.parametrize("cls", ["InvManagementBacklogEnv", "NetInvMgmtBacklogEnv"])
+def test_disabled_mode_horizon_raises_per_env(gpu, cls):
+    """After a masked reset the periods differ per env: the host cannot refuse
+    the overrun up front, so the step reports the kernels' per-env flag as the
+    reference's IndexError; the other envs' steps apply normally."""
+    import invsim
+    n = 100
+    env = getattr(invsim, cls)(n, device=gpu, autoreset_mode="disabled", record_demand=True)
+    env.reset(seed=0)
+    A = env.action_dim
+    a = torch.full((n, A), 5, dtype=env.act_dtype, device=gpu)
+    for _ in range(29):
+        env.step(a)
+    mask = torch.zeros(n, dtype=torch.bool, device=gpu)
+    mask[::2] = True
+    env.reset(options={"reset_mask": mask})   # even envs at t = 0, odd at t = 29
+    env.step(a)                               # odd envs reach the horizon: fine
+    with pytest.raises(IndexError):
+        env.step(a)                           # odd envs past it
+    assert env.status() == 0                  # the flag was reported and cleared
+    env.reset()
+    env.step(a)                               # lock-step again, no error
+
+
 def test_masked_reset(gpu, oracle):
     from invsim import InvManagementBacklogEnv
     n = 256
