@@ -176,7 +176,10 @@ int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, 
 
 /* Sticky device status word (bit 0: an env was stepped past its horizon with
  * autoreset disabled while the period was not lock-step; such steps are not
- * applied).  Synchronous.  clear != 0 resets it. */
+ * applied).  Synchronous.  clear != 0 resets it.  invsim_step / invsim_rollout /
+ * invsim_rollout_policy of an InvMgmt or NetInvMgmt handle in that state read it
+ * themselves (one stream sync) and return INVSIM_ERANGE ("...horizon...") after
+ * clearing it: the reference's IndexError (inventory_management.py:267). */
 int invsim_status(invsim_handle *h, uint32_t *flags, int32_t clear);
 
 /* ---- Closed-loop rollouts with an in-kernel heuristic agent.
