@@ -71,7 +71,7 @@ __device__ __forceinline__ void spec_demand(Pcg &g, const PtrsConst (&pc)[G::RL]
 // One step (:436-635) at period t < T given the step's market demands Dd; obs
 // row into orow (LDS).  Returns the reward; Rn receives R[t] (the fulfilled
 // orders) per link.
-template <class G>
+template <class G, bool WIN = true>
 __device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apow, NetSt<G> &s,
                                            const float (&act)[G::E], const double (&Dd)[G::RL], float *orow,
                                            double (&Rn)[G::E], double *met, double *irec) {
@@ -193,9 +193,11 @@ __device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apo
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
         if (G::L[k] == 0) continue;
+        if (WIN) {   // !WIN: another wave writes the older window entries
 #pragma unroll
-        for (int p = 0; p + 1 < G::L[k]; p++)
-            orow[G::win_off[k] + p] = (float)s.w[G::ring_off[k] + (G::L[k] - 1 - p) - 1];
+            for (int p = 0; p + 1 < G::L[k]; p++)
+                orow[G::win_off[k] + p] = (float)s.w[G::ring_off[k] + (G::L[k] - 1 - p) - 1];
+        }
         orow[G::win_off[k] + G::L[k] - 1] = (float)Rn[k];
     }
     (void)t;
@@ -425,6 +427,15 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     (void)t_start;
 }
 
+// Cross-wave LDS handoff inside a workgroup: orders LDS traffic only (an
+// __syncthreads() would also drain each wave's outstanding global loads and
+// stores, s_waitcnt vmcnt(0), before the s_barrier)
+__device__ __forceinline__ void net_wg_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Single lock-step step (invsim_step: K = 1, t < T, no policy, no SAME_STEP
 // reset in this step) with the demand lookahead.  The market demands of a step
 // are Poisson draws of the env's own stream at fixed rates, and reset() draws
@@ -578,6 +589,178 @@ net_step1_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
     }
 }
 
+// net_step1_kernel with the work of 64 envs split over two waves of one
+// workgroup (the step's load -> compute -> store chain is the step time at the
+// 32 768-env configuration):
+//   wave 0 (window)   the observation's order windows: R[t-a] for ages
+//                     1 .. L-1 of every link (52 of the default graph's 61
+//                     ring entries), read, rounded to f32 and placed in the
+//                     LDS tile
+//   wave 1 (dynamics) X, U, Y, the arrivals (age L), actions and demands; the
+//                     step with the tile's U, X and newest orders; the state,
+//                     ring slot and output stores (and the inline draw /
+//                     lookahead production when !HIT)
+// Then both waves store half of the tile.  Lookahead workgroups (HIT) cover 128
+// envs, one per thread.  Same arithmetic as net_spec_kernel.
+template <class G, bool HIT>
+__global__ void __launch_bounds__(2 * WAVE)
+net_step2_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) {
+    extern __shared__ __attribute__((aligned(16))) float ns_lds[];
+    constexpr int O = G::O, RL = G::RL, NR = 2 + G::RL;
+    constexpr int NT = RHS_LDS_MAX / WAVE;
+    constexpr int HALF_IT = (EPW * O * 4 / 2 + 16 * WAVE - 1) / (16 * WAVE) + 1;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    const uint64_t *Acur = P.ahead + (int64_t)cur * NR * S;
+    uint64_t *Anxt = P.ahead + (int64_t)(cur ^ 1) * NR * S;
+    double *rhs_l = reinterpret_cast<double *>(ns_lds + ((EPW * O + 3) / 4) * 4);
+    PtrsConst pc[RL];
+#pragma unroll
+    for (int r = 0; r < RL; r++) pc[r] = P.rl_pc[r];
+    auto stage = [&](double (&tv)[RL][NT]) {
+#pragma unroll
+        for (int r = 0; r < RL; r++) {
+            const int qm = pc[r].nk > 0 ? pc[r].nk - 1 : 0;
+            const double *src = pc[r].nk > 0 ? P.rhs + pc[r].toff : P.alpha_pow;   // any valid pointer
+#pragma unroll
+            for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
+        }
+    };
+    auto flush = [&](const double (&tv)[RL][NT]) {   // each wave writes the whole (identical) table
+#pragma unroll
+        for (int r = 0; r < RL; r++)
+#pragma unroll
+            for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
+        wave_lds_sync();
+    };
+    const int bid = (int)blockIdx.x;
+    if (HIT && bid < gla) {   // ---- lookahead workgroup: 128 envs, one per thread
+        const int64_t e = (int64_t)bid * (2 * WAVE) + threadIdx.x;
+        const bool valid = e < N;
+        const int64_t el = valid ? e : N - 1;
+        double tv[RL][NT];
+        stage(tv);
+        Pcg g;
+        g.hi = Acur[el];
+        g.lo = Acur[S + el];
+        g.inc_hi = P.cm.rng.inc_hi[el];
+        g.inc_lo = P.cm.rng.inc_lo[el];
+        flush(tv);
+        double Dd[RL];
+        spec_demand<G>(g, pc, rhs_l, Dd);
+        if (valid) {
+            st_store(Anxt + e, g.hi);
+            st_store(Anxt + S + e, g.lo);
+#pragma unroll
+            for (int r = 0; r < RL; r++) st_store(Anxt + (2 + r) * S + e, (uint64_t)(int64_t)Dd[r]);
+        }
+        return;
+    }
+    const int64_t e0 = (int64_t)(bid - (HIT ? gla : 0)) * EPW;
+    const int64_t e = e0 + lane;
+    const bool valid = e < N;
+    const int nvalid = (int)((N - e0) < EPW ? (N - e0) : EPW);
+    const int64_t el = valid ? e : N - 1;      // lanes past N mirror env N-1 (loads only)
+    float *tile = ns_lds;
+    float *trow = tile + lane * O;
+    const int64_t tcount = (int64_t)nvalid * O;
+    const int64_t thalf = ((tcount / 2) + 3) & ~(int64_t)3;           // 16-B aligned split
+    const int64_t h = thalf < tcount ? thalf : tcount;
+    if (threadIdx.x < WAVE) {   // ---- window wave
+        float wf[G::sumL > 0 ? G::sumL : 1];
+#pragma unroll
+        for (int k = 0; k < G::E; k++) {
+            if (G::L[k] < 2) continue;
+#pragma unroll
+            for (int a = 1; a < G::L[k]; a++) {
+                const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+                const double v = P.Rring[(int64_t)row * S + el];
+                wf[G::ring_off[k] + a - 1] = (t - a >= 0) ? (float)v : 0.f;   // zeroed history (:315-321)
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < G::E; k++) {
+            if (G::L[k] < 2) continue;
+#pragma unroll
+            for (int p = 0; p + 1 < G::L[k]; p++) trow[G::win_off[k] + p] = wf[G::ring_off[k] + (G::L[k] - 1 - p) - 1];
+        }
+        net_wg_sync();   // tile complete
+        store_tile<HALF_IT>(tile, io.obs + e0 * O, h, lane);
+        return;
+    }
+    // ---- dynamics wave
+    NetSt<G> st;
+    double Dd[RL];
+    double tv[RL][NT];
+    if (HIT) {
+#pragma unroll
+        for (int r = 0; r < RL; r++) Dd[r] = (double)(int64_t)Acur[(2 + r) * S + el];
+    } else {
+        stage(tv);
+        st.g = P.cm.rng.load(el);
+    }
+    const double apow = P.alpha_pow[t];
+#pragma unroll
+    for (int j = 0; j < G::J; j++) st.X[j] = P.X[j * S + el];
+#pragma unroll
+    for (int r = 0; r < RL; r++) st.U[r] = P.U[r * S + el];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) st.Y[k] = P.Y[k * S + el];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) {   // only the arrivals: age L = R[t - L]
+        if (G::L[k] == 0) continue;
+        const int a = G::L[k];
+        const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+        const double v = P.Rring[(int64_t)row * S + el];
+        st.w[G::ring_off[k] + a - 1] = (t - a >= 0) ? v : 0.0;
+    }
+    float act[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) act[k] = io.act[el * G::E + k];
+    if (!HIT) {
+        flush(tv);
+        spec_demand<G>(st.g, pc, rhs_l, Dd);                   // :536-541
+    }
+    double Rn[G::E];
+    double *irec = (valid && P.cm.info_rec) ? (double *)P.cm.info_rec + e * (2 * RL + 2 * G::J + 2 * G::E) : nullptr;
+    const double r = spec_dyn<G, false>(P, t, apow, st, act, Dd, trow, Rn, nullptr, irec);
+    net_wg_sync();   // tile complete
+    if (h < tcount) store_tile<HALF_IT>(tile + h, io.obs + e0 * O + h, tcount - h, lane);
+    if (valid) {
+        out_store(io.rew + e, r);
+        out_store(io.term + e, (uint8_t)0);
+        out_store(io.trunc + e, (uint8_t)(t + 1 >= P.T ? 1 : 0));
+        if (P.cm.info_demand) {
+#pragma unroll
+            for (int q = 0; q < RL; q++) P.cm.info_demand[e * RL + q] = (int64_t)Dd[q];
+        }
+#pragma unroll
+        for (int k = 0; k < G::E; k++)
+            if (G::L[k] > 0)
+                st_store(P.Rring + (int64_t)(G::ring_off[k] + (int)((uint32_t)t % (uint32_t)G::L[k])) * S + e, Rn[k]);
+#pragma unroll
+        for (int j = 0; j < G::J; j++) st_store(P.X + j * S + e, st.X[j]);
+#pragma unroll
+        for (int q = 0; q < RL; q++) st_store(P.U + q * S + e, st.U[q]);
+#pragma unroll
+        for (int k = 0; k < G::E; k++) st_store(P.Y + k * S + e, st.Y[k]);
+    }
+    if (!HIT) {   // committed state (after this step's draws) -> slot cur; the lookahead -> slot cur ^ 1
+        if (valid) {
+            st_store((uint64_t *)Acur + e, st.g.hi);
+            st_store((uint64_t *)Acur + S + e, st.g.lo);
+        }
+        spec_demand<G>(st.g, pc, rhs_l, Dd);
+        if (valid) {
+            st_store(Anxt + e, st.g.hi);
+            st_store(Anxt + S + e, st.g.lo);
+#pragma unroll
+            for (int q = 0; q < RL; q++) st_store(Anxt + (2 + q) * S + e, (uint64_t)(int64_t)Dd[q]);
+        }
+    }
+}
+
 // cm.rng <- the committed slot of the lookahead cache
 __global__ void __launch_bounds__(256) net_commit_kernel(NetParams P, int slot, int nr) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -588,14 +771,6 @@ __global__ void __launch_bounds__(256) net_commit_kernel(NetParams P, int slot, 
     P.cm.rng.lo[e] = A[S + e];
 }
 
-// Cross-wave LDS handoff inside a workgroup: orders LDS traffic only (an
-// __syncthreads() would also drain each wave's outstanding global loads and
-// stores, s_waitcnt vmcnt(0), before the s_barrier)
-__device__ __forceinline__ void net_wg_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 // K-step lock-step rollout (invsim_rollout without a policy, NEXT_STEP
 // autoreset or no overrun, Poisson market demand) of a compiled network, one
@@ -828,6 +1003,12 @@ static size_t spec_lds_bytes() {
     return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float) + (size_t)G::RL * RHS_LDS_MAX * sizeof(double);
 }
 
+// INVSIM_NET_SPLIT=0 keeps the step on the one-wave net_step1_kernel (A/B, tests)
+static bool net_split_enabled() {
+    const char *v = getenv("INVSIM_NET_SPLIT");
+    return !(v && v[0] == '0');
+}
+
 // INVSIM_NET_AHEAD=0 turns the step's demand lookahead off (A/B measurements)
 static bool net_ahead_enabled() {
     const char *v = getenv("INVSIM_NET_AHEAD");
@@ -846,8 +1027,15 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
         const bool hit = ahead;
         const int gla = hit ? (int)((p.cm.N + WAVE - 1) / WAVE) : 0;
         const dim3 grid2(grid.x + gla);
-        if (hit) hipLaunchKernelGGL((net_step1_kernel<G, true>), grid2, block, lds, s, p, t_u, io, slot, gla);
-        else hipLaunchKernelGGL((net_step1_kernel<G, false>), grid2, block, lds, s, p, t_u, io, slot, gla);
+        if (net_split_enabled()) {
+            const int gl2 = hit ? (int)((p.cm.N + 2 * WAVE - 1) / (2 * WAVE)) : 0;
+            const dim3 g2(grid.x + gl2), b2(2 * WAVE);
+            if (hit) hipLaunchKernelGGL((net_step2_kernel<G, true>), g2, b2, lds, s, p, t_u, io, slot, gl2);
+            else hipLaunchKernelGGL((net_step2_kernel<G, false>), g2, b2, lds, s, p, t_u, io, slot, gl2);
+        } else {
+            if (hit) hipLaunchKernelGGL((net_step1_kernel<G, true>), grid2, block, lds, s, p, t_u, io, slot, gla);
+            else hipLaunchKernelGGL((net_step1_kernel<G, false>), grid2, block, lds, s, p, t_u, io, slot, gla);
+        }
         ahead = true;
         slot ^= 1;
         return hipGetLastError();

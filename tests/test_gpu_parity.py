@@ -986,3 +986,32 @@ def test_newsvendor_rollout_sampler_mixes(gpu, monkeypatch, mu_max, step_limit):
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
     monkeypatch.delenv("INVSIM_NV_ROLL")
+
+
+@pytest.mark.parametrize("graph,n", [("default", 1000), ("custom", 777), ("default", 32768)])
+def test_net_two_wave_step_equals_one_wave(gpu, monkeypatch, graph, n):
+    """Lock-step steps of a compiled network run net_step2_kernel (order windows
+    on one wave, dynamics on the other); INVSIM_NET_SPLIT=0 keeps
+    net_step1_kernel.  Identical outputs, demands, step records and state
+    across episodes."""
+    import invsim
+    from invsim.topology import custom_graph, default_graph
+    mk_g = default_graph if graph == "default" else custom_graph
+    envs = [invsim.NetInvMgmtBacklogEnv(n, device=gpu, graph=mk_g(), record_demand=True, record_info=True)
+            for _ in range(2)]
+    for env in envs:
+        env.reset(seed=9)
+    g = torch.Generator(device=gpu).manual_seed(4)
+    A = envs[0].action_dim
+    for k in range(65):
+        a = torch.rand((n, A), device=gpu, generator=g) * 250 - 5
+        outs = []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_NET_SPLIT", "1" if i == 0 else "0")
+            o, r, te, tr, info = env.step(a)
+            outs.append([o.clone(), r.clone(), tr.clone(), env._demand.clone()]
+                        + [v.clone() for v in info.values() if torch.is_tensor(v)])
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), k
+    assert torch.equal(envs[0].get_state(), envs[1].get_state())
+    monkeypatch.delenv("INVSIM_NET_SPLIT")
