@@ -276,10 +276,15 @@ int invsim_create_newsvendor(const invsim_newsvendor_spec *spec, int64_t n, int3
         p.par = at<double>(h, o_par);
         p.pipe = at<float>(h, o_pipe);
         p.ahead = nullptr;
-        {   // demand lookahead cache: 2 slots x 3 rows x Npad u64
-            hipError_t e = hipMalloc(&h->scratch, (size_t)(2 * 3 * h->Npad * sizeof(uint64_t)));
-            if (e != hipSuccess) rc = fail(h, INVSIM_ENOMEM, "hipMalloc(lookahead cache)");
-            else p.ahead = static_cast<uint64_t *>(h->scratch);
+        p.pcon = nullptr;
+        {   // demand lookahead cache: 2 slots x 3 rows x Npad u64, then 6 rows of Poisson constants
+            hipError_t e = hipMalloc(&h->scratch, (size_t)((2 * 3 + 6) * h->Npad * sizeof(uint64_t)));
+            if (e != hipSuccess) {
+                rc = fail(h, INVSIM_ENOMEM, "hipMalloc(lookahead cache)");
+            } else {
+                p.ahead = static_cast<uint64_t *>(h->scratch);
+                p.pcon = reinterpret_cast<double *>(p.ahead + 2 * 3 * h->Npad);
+            }
         }
         h->past_ok = true;
         if (rc == INVSIM_OK) rc = init_period(h, std::max(spec->step_limit, 0));

@@ -62,8 +62,11 @@ struct NvParams {
     const double *lgtab; // [RHS_LDS_MAX] loggam(k + 1), host (numpy's formula)
     float *pipe;         // [L][Npad]  order ring, slot = step index mod L
     // demand lookahead cache (not part of the state blob): two slots of rows
-    // [state hi, state lo, next demand] x Npad (nv_step1_kernel)
+    // [state hi, state lo, next demand] x Npad (nv_step1_kernel), and the
+    // episode's Poisson constants of every env, written by the launch that
+    // starts a lookahead chain (mu is fixed while a chain runs)
     uint64_t *ahead;
+    double *pcon;        // [6][Npad]  a, b, vr, loglam, log_invalpha, enlam
 };
 
 // ---------------------------------------------------------------- InvMgmt

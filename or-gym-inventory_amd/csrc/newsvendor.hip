@@ -488,6 +488,32 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     TPROBE(5);
 }
 
+// numpy random_poisson's constants of a per-env rate, computed once per episode
+// (np_poisson_dyn recomputes them per draw)
+__device__ __forceinline__ PtrsConst nv_rate_const(double lam) {
+    PtrsConst c;
+    c.lam = lam;
+    c.slam = sqrt(lam);
+    c.loglam = log(lam);
+    c.b = 0.931 + 2.53 * c.slam;
+    c.a = -0.059 + 0.02483 * c.b;
+    c.invalpha = 1.1239 + 1.1328 / (c.b - 3.4);
+    c.vr = 0.9277 - 3.6224 / (c.b - 2);
+    c.log_invalpha = log(c.invalpha);
+    c.a2 = 2 * c.a;
+    c.enlam = exp(-lam);
+    c.k0 = 0;
+    c.nk = 0;
+    return c;
+}
+
+// np_poisson_dyn with the episode's constants (same draws, same arithmetic)
+__device__ __forceinline__ int64_t nv_poisson_c(Pcg &g, const PtrsConst &c, const double *lgtab) {
+    if (c.lam >= 10) return np_poisson_ptrs_lg(g, c, lgtab, RHS_LDS_MAX);
+    if (c.lam == 0) return 0;
+    return np_poisson_mult(g, c.enlam);
+}
+
 // Single lock-step step (invsim_step: K = 1, t_u < step_limit, no policy, not a
 // SAME_STEP done step) with the demand lookahead.  The demand of a step is
 // Poisson(mu) of the env's own stream, and mu is fixed for the episode, so the
@@ -541,7 +567,19 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
             }
             const bool mine = mult_wg == (mu < 10 && mu != 0);
             if (mine) {
-                const int64_t dn = env_poisson_dyn(g, mu, lg_l, RHS_LDS_MAX);
+                // the chain's constants (nv_rate_const(mu), stored by its first launch)
+                PtrsConst c;
+                c.lam = mu;
+                c.a = P.pcon[el];
+                c.b = P.pcon[S + el];
+                c.vr = P.pcon[2 * S + el];
+                c.loglam = P.pcon[3 * S + el];
+                c.log_invalpha = P.pcon[4 * S + el];
+                c.enlam = P.pcon[5 * S + el];
+                c.a2 = 2 * c.a;
+                c.k0 = 0;
+                c.nk = 0;
+                const int64_t dn = nv_poisson_c(g, c, lg_l);
                 if (valid) {
                     st_store(Anxt + e, g.hi);
                     st_store(Anxt + S + e, g.lo);
@@ -584,8 +622,22 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
         }
     }
     const float act = io.act[el];
+    PtrsConst c;
+    if (!HIT) {   // this launch starts a lookahead chain: the episode's constants, once
+        c = nv_rate_const(st.par[4]);
+        ts.flush(lane);
+        dpre = nv_poisson_c(st.g, c, lg_l);                                // :146
+        if (valid) {
+            st_store(P.pcon + e, c.a);
+            st_store(P.pcon + S + e, c.b);
+            st_store(P.pcon + 2 * S + e, c.vr);
+            st_store(P.pcon + 3 * S + e, c.loglam);
+            st_store(P.pcon + 4 * S + e, c.log_invalpha);
+            st_store(P.pcon + 5 * S + e, c.enlam);
+        }
+    }
     double r;
-    const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, lg_l, HIT ? nullptr : &ts, r,
+    const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, lg_l, nullptr, r,
                                      valid ? P.cm.info_demand : nullptr, dpre);
     if (valid) {
         out_store(io.rew + e, r);
@@ -599,39 +651,13 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
             st_store((uint64_t *)Acur + e, st.g.hi);
             st_store((uint64_t *)Acur + S + e, st.g.lo);
         }
-        const int64_t dn = env_poisson_dyn(st.g, st.par[4], lg_l, RHS_LDS_MAX);
+        const int64_t dn = nv_poisson_c(st.g, c, lg_l);
         if (valid) {
             st_store(Anxt + e, st.g.hi);
             st_store(Anxt + S + e, st.g.lo);
             st_store(Anxt + 2 * S + e, (uint64_t)dn);
         }
     }
-}
-
-// numpy random_poisson's constants of a per-env rate, computed once per episode
-// (np_poisson_dyn recomputes them per draw)
-__device__ __forceinline__ PtrsConst nv_rate_const(double lam) {
-    PtrsConst c;
-    c.lam = lam;
-    c.slam = sqrt(lam);
-    c.loglam = log(lam);
-    c.b = 0.931 + 2.53 * c.slam;
-    c.a = -0.059 + 0.02483 * c.b;
-    c.invalpha = 1.1239 + 1.1328 / (c.b - 3.4);
-    c.vr = 0.9277 - 3.6224 / (c.b - 2);
-    c.log_invalpha = log(c.invalpha);
-    c.a2 = 2 * c.a;
-    c.enlam = exp(-lam);
-    c.k0 = 0;
-    c.nk = 0;
-    return c;
-}
-
-// np_poisson_dyn with the episode's constants (same draws, same arithmetic)
-__device__ __forceinline__ int64_t nv_poisson_c(Pcg &g, const PtrsConst &c, const double *lgtab) {
-    if (c.lam >= 10) return np_poisson_ptrs_lg(g, c, lgtab, RHS_LDS_MAX);
-    if (c.lam == 0) return 0;
-    return np_poisson_mult(g, c.enlam);
 }
 
 __device__ __forceinline__ void nv_wg_sync() {
