@@ -387,9 +387,11 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     NvState<LT> st;
     st.g = P.cm.rng.load(el);
     int sc = TU ? t_u : P.cm.period[el];
-    if (ONE && TU && sc >= P.step_limit) {
-        // lock-step NEXT_STEP autoreset of the whole batch (DISABLED overruns are
-        // refused by the host when lock-step; SAME_STEP resets in the done step)
+    if (ONE && TU && sc >= P.step_limit && P.cm.autoreset == AR_NEXT_STEP) {
+        // lock-step NEXT_STEP autoreset of the whole batch.  DISABLED keeps stepping
+        // the same episode past step_limit with truncated=True (newsvendor.py:190
+        // has no horizon check; the oracle does the same, oracle.c nv_step), and
+        // SAME_STEP resets in the done step, so neither reaches this branch
         nv_reset_regs<LT>(P, e, st, trow, valid);
         if (valid) {
             out_store(io.rew + e, 0.0);

@@ -29,20 +29,39 @@ except Exception:  # noqa: BLE001
 class InvSimVecEnv(_SB3VecEnv):
     def __init__(self, env_cls, n_envs, env_config=None, device=None, seed=None):
         self.venv = env_cls(num_envs=n_envs, device=device, autoreset_mode="same_step", **(env_config or {}))
+        if _SB3VecEnv is not object:   # SB3 2.x: sets reset_infos, _seeds, _options, render_mode
+            super().__init__(n_envs, self.venv.single_observation_space, self.venv.single_action_space)
         self.num_envs = n_envs
         self.observation_space = self.venv.single_observation_space
         self.action_space = self.venv.single_action_space
         self.render_mode = None
+        # SB3 2.x VecEnv state (also kept when SB3 is absent, so callers that
+        # read them behave the same): per-env reset infos, pending seeds/options
+        self.reset_infos = [{} for _ in range(n_envs)]
+        self._seeds = [None for _ in range(n_envs)]
+        self._options = [{} for _ in range(n_envs)]
         self._seed = seed
         self._actions = None
         self._obs = None
 
     # -- VecEnv protocol ------------------------------------------------------
     def reset(self):
-        obs, _ = self.venv.reset(seed=self._seed)
+        obs, info = self.venv.reset(seed=self._seed)
         self._seed = None
+        self._seeds = [None for _ in range(self.num_envs)]
+        self._options = [{} for _ in range(self.num_envs)]
+        self.reset_infos = [dict(info) for _ in range(self.num_envs)]
         self._obs = obs
         return obs.cpu().numpy()
+
+    def set_options(self, options=None):
+        """SB3 2.x: options for the next reset (one dict, or one per env).  The
+        reference envs ignore reset options, so they are only recorded."""
+        if options is None:
+            options = {}
+        if isinstance(options, dict):
+            options = [dict(options) for _ in range(self.num_envs)]
+        self._options = list(options)
 
     def step_async(self, actions):
         self._actions = actions
@@ -71,7 +90,8 @@ class InvSimVecEnv(_SB3VecEnv):
 
     def seed(self, seed=None):
         self._seed = seed
-        return [None if seed is None else seed + i for i in range(self.num_envs)]
+        self._seeds = [None if seed is None else seed + i for i in range(self.num_envs)]
+        return list(self._seeds)
 
     def _indices(self, indices):
         if indices is None:

@@ -156,6 +156,44 @@ def test_newsvendor_vs_oracle_65536(gpu, oracle):
         assert np.array_equal(tr.cpu().numpy(), e_tr)
 
 
+@pytest.mark.parametrize("ahead", ["1", "0"])
+def test_newsvendor_disabled_past_step_limit_vs_oracle(gpu, oracle, monkeypatch, ahead):
+    """DISABLED autoreset: newsvendor.py:125-204 has no horizon check, so steps
+    past step_limit keep stepping the same episode (same params, no reset
+    draws) with truncated=True.  step() and rollout() over the same span agree
+    with the C oracle on obs, reward bits, truncation, demand and params."""
+    from invsim import NewsvendorEnv
+    monkeypatch.setenv("INVSIM_NV_AHEAD", ahead)
+    n, limit, T = 1000, 7, 13
+    mk = lambda: NewsvendorEnv(n, device=gpu, step_limit=limit, autoreset_mode="disabled",  # noqa: E731
+                               record_demand=True)
+    env, env_r = mk(), mk()
+    orc = oracle.OracleNewsvendor(n, step_limit=limit)
+    orc.seed(range(500, 500 + n))
+    e_obs = orc.reset()
+    obs, _ = env.reset(seed=500)
+    env_r.reset(seed=500)
+    assert _eq_bits(obs.cpu().numpy(), e_obs)
+    rng = np.random.default_rng(77)
+    acts = rng.uniform(-50, 2500, size=(T, n, 1)).astype(np.float32)
+    for s in range(T):
+        o, r, te, tr, info = env.step(torch.from_numpy(acts[s]).to(gpu))
+        e_obs, e_rew, e_tr, e_dem = orc.step(acts[s])
+        assert np.array_equal(info["demand"].cpu().numpy(), e_dem), f"demand step {s}"
+        assert _eq_bits(o.cpu().numpy(), e_obs), f"obs step {s}"
+        _assert_reward(r.cpu().numpy(), e_rew, f"step {s}")
+        assert np.array_equal(tr.cpu().numpy(), e_tr), f"truncated step {s}"
+        assert bool(tr.all()) == (s + 1 >= limit)
+    assert _eq_bits(env.params().cpu().numpy(), orc.params())
+    ro, rr, rte, rtr = env_r.rollout(torch.from_numpy(acts).to(gpu))[:4]
+    assert _eq_bits(ro[-1].cpu().numpy(), e_obs)
+    _assert_reward(rr[-1].cpu().numpy(), e_rew, "rollout last step")
+    assert bool(rtr[limit - 1:].all()) and not rtr[:limit - 1].any()
+    fa, fb = env.state_fields(), env_r.state_fields()
+    for k in ("rng", "params", "pipeline"):
+        assert torch.equal(fa[k], fb[k]), k
+
+
 @pytest.mark.parametrize("graph", ["default", "custom"])
 def test_net_vs_oracle_4096(gpu, oracle, graph):
     from invsim import NetInvMgmtBacklogEnv

@@ -1,0 +1,76 @@
+"""Fixed cost of bench.py's timed region at small K (the driver runs --steps 20).
+
+Times, on the InvMgmt Backlog 65 536-env step, K back-to-back invsim_step
+launches bracketed the way bench.py does (synchronize, t0, K launches,
+synchronize), against variants of the closing wait, and the empty region.
+Prints one line per variant: wall us per region, kernel-event us, K.
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "or-gym-inventory_amd"))
+
+import torch  # noqa: E402
+
+import invsim  # noqa: E402
+from invsim import _capi  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    env = invsim.InvManagementBacklogEnv(65536, device=dev, copy=False)
+    env.reset(seed=0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    hi = torch.tensor([101.0, 201.0, 231.0], device=dev, dtype=torch.float64)
+    acts = [torch.floor(torch.rand((65536, 3), device=dev, dtype=torch.float64, generator=g) * hi).to(torch.int64)
+            for _ in range(16)]
+    N, O = 65536, env.obs_dim
+    obs = torch.empty((N, O), dtype=torch.int64, device=dev)
+    rew = torch.empty(N, dtype=torch.float64, device=dev)
+    te = torch.empty(N, dtype=torch.bool, device=dev)
+    tr = torch.empty(N, dtype=torch.bool, device=dev)
+    lib, h = env._lib, env._h
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    ptrs = [a.data_ptr() for a in acts]
+    po, pr, pt, pu = obs.data_ptr(), rew.data_ptr(), te.data_ptr(), tr.data_ptr()
+    hip = _capi.C.CDLL("libamdhip64.so")
+
+    def region(K, wait):
+        torch.cuda.synchronize(dev)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for i in range(K):
+            lib.invsim_step(h, ptrs[i % 16], po, pr, pt, pu, None, sp)
+        e1.record(stream)
+        if wait == "sync":
+            torch.cuda.synchronize(dev)
+        elif wait == "spin":
+            while not e1.query():
+                pass
+            torch.cuda.synchronize(dev)
+        elif wait == "stream":
+            hip.hipStreamSynchronize(_capi.C.c_void_p(sp))
+            torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        return el * 1e6, e0.elapsed_time(e1) * 1e3
+
+    for _ in range(50):
+        region(20, "sync")
+    for K in (0, 1, 20, 200, 2000):
+        for wait in ("sync", "spin", "stream"):
+            w, k = zip(*[region(K, wait) for _ in range(15)])
+            w, k = sorted(w), sorted(k)
+            print(f"K={K:5d} wait={wait:6s} wall_us med={w[7]:9.1f} min={w[0]:9.1f}  "
+                  f"events_us med={k[7]:9.1f}  per-step wall={w[7] / max(K, 1):7.2f} ev={k[7] / max(K, 1):7.2f}",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
