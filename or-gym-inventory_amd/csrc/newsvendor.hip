@@ -688,6 +688,118 @@ __device__ __forceinline__ void nv_chunk(int t, int rem, int step_limit, bool nx
     }
 }
 
+// numpy random_poisson_mult draws of one rollout chunk for the multiplication
+// wave's envs (0 < lam < 10: ~5 % of envs at the default mu_max, a few per
+// workgroup), G lanes per env.  The sequential sampler costs one PCG64 step
+// (a 128-bit multiply) per uniform and lam + 1 uniforms per draw on the
+// wave's critical path; here the G lanes of an env's group compute the next G
+// uniforms of its stream at once by jump-ahead (lane jl: state after jl + 1
+// LCG steps = A_{jl+1} s + S_{jl+1} inc, group_rng.hpp), then every lane of
+// the group runs the product chain over them in stream order -- the same
+// roundings, comparisons and draw boundaries as numpy (a round's uniforms can
+// finish one draw and start the next) -- and the group's base state advances
+// by the uniforms actually consumed.  Owners (lanes with `own`) hand their
+// generator to the group and get it back advanced; the group's first lane
+// writes the draws into the owner's column of `dcol` ([CH][WAVE]).
+// G = 16, 8 or 4 for up to 4, 8 or 16 envs; more than 16 envs (small mu_max)
+// keep the one-lane sequential sampler (the caller's fallback): returns false.
+__device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own, int nd, int64_t *dcol,
+                                                  double *ubuf, const uint64_t *jt, int lane) {
+    const uint64_t mm = (uint64_t)__ballot(own && nd > 0);
+    const int nm = __popcll(mm);
+    if (nm > 16) return false;
+    if (nm == 0) return true;
+    const int lg = nm > 8 ? 2 : nm > 4 ? 3 : 4;          // log2 G
+    const int G = 1 << lg;
+    const int grp = lane >> lg, jl = lane & (G - 1), gbase = grp << lg;
+    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+    int *slot = reinterpret_cast<int *>(ubuf);
+    if (own && nd > 0) slot[rank] = lane;                // owner lane of group `rank`
+    wave_lds_sync();
+    const bool act = grp < nm;
+    const int src = act ? slot[grp] : lane;
+    wave_lds_sync();
+    Pcg s;
+    s.hi = shfl_u64(g.hi, src);
+    s.lo = shfl_u64(g.lo, src);
+    s.inc_hi = shfl_u64(g.inc_hi, src);
+    s.inc_lo = shfl_u64(g.inc_lo, src);
+    const double en = __shfl(enlam, src);
+    // jt: the jump table (group_rng.hpp) staged in LDS, rows a_hi, a_lo, s_hi, s_lo
+    const uint64_t ah = jt[jl + 1], al = jt[(JUMP_MAX + 1) + jl + 1];
+    uint64_t sih, sil;
+    mul128(jt[2 * (JUMP_MAX + 1) + jl + 1], jt[3 * (JUMP_MAX + 1) + jl + 1], s.inc_hi, s.inc_lo, sih, sil);
+    int j = act ? 0 : nd;
+    int X = 0;
+    double prod = 1.0;
+    while (__ballot(j < nd)) {
+        const bool live = j < nd;
+        uint64_t th, tl;
+        mul128(ah, al, s.hi, s.lo, th, tl);
+        const uint64_t lo = tl + sil;
+        th = th + sih + (lo < tl ? 1ULL : 0ULL);
+        tl = lo;
+        const uint64_t x = th ^ tl;
+        const unsigned rot = (unsigned)(th >> 58);
+        const uint64_t o = (x >> rot) | (x << ((64u - rot) & 63u));
+        ubuf[lane] = (double)(o >> 11) * (1.0 / 9007199254740992.0);
+        wave_lds_sync();
+        // the product chain over the round's uniforms in stream order (4 loaded
+        // at a time; G is a multiple of 4): prod, and a bit per uniform that
+        // ends a draw (prod <= enlam); then the draws, in order, from the bits
+        uint32_t stops = 0;
+        for (int q0 = 0; q0 < G; q0 += 4) {
+            double u[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) u[q] = ubuf[gbase + q0 + q];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const double pq = prod * u[q];
+                const bool cont = pq > en;
+                prod = cont ? pq : 1.0;
+                stops |= cont ? 0u : (1u << (q0 + q));
+            }
+        }
+        int need = live ? nd - j : 0;
+        int used = G, last = -1;
+        while (__ballot(stops != 0 && need > 0)) {
+            if (stops != 0 && need > 0) {
+                const int pos = __builtin_ctz(stops);
+                if (jl == 0) dcol[j * WAVE + src] = (int64_t)(last < 0 ? X + pos : pos - last - 1);
+                j++;
+                need--;
+                last = pos;
+                stops &= stops - 1;
+                if (need == 0) used = pos + 1;
+            }
+        }
+        if (live) {
+            if (j == nd) {          // the chunk's draws are done: the next starts fresh
+                X = 0;
+                prod = 1.0;
+            } else {
+                X = last < 0 ? X + G : G - 1 - last;
+            }
+        }
+        wave_lds_sync();
+        const uint64_t nh = shfl_u64(th, gbase + used - 1);
+        const uint64_t nl = shfl_u64(tl, gbase + used - 1);
+        if (live) {
+            s.hi = nh;
+            s.lo = nl;
+        }
+    }
+    // the advanced generator back to its owner (group `rank` -> lane rank * G)
+    const int back = (own && nd > 0) ? (rank << lg) : lane;
+    const uint64_t bh = shfl_u64(s.hi, back), bl = shfl_u64(s.lo, back);
+    if (own && nd > 0) {
+        g.hi = bh;
+        g.lo = bl;
+    }
+    return true;
+}
+
 // K-step lock-step rollout (invsim_rollout without a policy, NEXT_STEP or
 // DISABLED autoreset, compile-time lead time LT > 0), one 192-thread workgroup
 // per 64 envs:
@@ -719,7 +831,8 @@ struct NvRoll {
     static constexpr size_t tile_bytes() { return (size_t)((EPW * O + 3) / 4) * 4 * sizeof(float); }
     static constexpr size_t lds() {
         return tile_bytes() + RHS_LDS_MAX * sizeof(double) + 2 * (size_t)CH * WAVE * sizeof(int64_t) +
-               2 * NP * (size_t)WAVE * sizeof(double);
+               2 * NP * (size_t)WAVE * sizeof(double) + (size_t)WAVE * sizeof(double) +
+               4 * (JUMP_MAX + 1) * sizeof(uint64_t);
     }
 };
 
@@ -734,6 +847,8 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
     double *lg_l = reinterpret_cast<double *>(nr_lds + R::tile_bytes() / sizeof(float));
     int64_t *dbuf = reinterpret_cast<int64_t *>(lg_l + RHS_LDS_MAX);     // [2][CH][WAVE]
     double *pbuf = reinterpret_cast<double *>(dbuf + 2 * CH * WAVE);      // [2][NP][WAVE]
+    double *ubuf = pbuf + 2 * NP * WAVE;                                   // [WAVE] mult wave's uniforms
+    uint64_t *jt = reinterpret_cast<uint64_t *>(ubuf + WAVE);              // [4][JUMP_MAX + 1] jump table
     const int lane = threadIdx.x & (WAVE - 1);
     const int role = threadIdx.x / WAVE;
     const int64_t N = P.cm.N;
@@ -751,6 +866,9 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
         if (!multw) {
             ts.dst = lg_l;
             ts.load(P.lgtab, RHS_LDS_MAX, lane);
+        } else {
+            const uint64_t *jsrc = &c_jump.a_hi[0];   // the four rows are contiguous
+            for (int q = lane; q < 4 * (JUMP_MAX + 1); q += WAVE) jt[q] = jsrc[q];
         }
         NvState<LT> st;
         st.g = P.cm.rng.load(el);
@@ -765,9 +883,18 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
             nv_chunk(t, K - k0, P.step_limit, nxt, CH, len, rs);
             const int nd = mine ? len - (rs ? 1 : 0) : 0;    // draws of this lane (the reset step draws none)
             int64_t *db = dbuf + cb * CH * WAVE + lane;
-#ifdef INVSIM_ABL_ROLL_NO_DRAW
+#if defined(INVSIM_ABL_ROLL_NO_DRAW)
             for (int j = 0; j < nd; j++) db[j * WAVE] = 20;
 #else
+#if defined(INVSIM_ABL_ROLL_NO_MULT) || defined(INVSIM_ABL_ROLL_NO_PTRS)
+#ifdef INVSIM_ABL_ROLL_NO_MULT
+            if (multw) {
+#else
+            if (!multw) {
+#endif
+                for (int j = 0; j < nd; j++) db[j * WAVE] = 5;
+            } else
+#endif
             if (!multw) {
                 if (c.lam == 0) {
                     for (int j = 0; j < nd; j++) db[j * WAVE] = 0;
@@ -791,8 +918,9 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
                         }
                     }
                 }
-            } else {
-                // numpy random_poisson_mult, one uniform per iteration, lanes independent
+            } else if (!nv_mult_chunk_grp(st.g, c.enlam, mine, len - (rs ? 1 : 0), dbuf + cb * CH * WAVE, ubuf, jt, lane)) {
+                // more than 16 envs on this branch: numpy random_poisson_mult, one
+                // uniform per iteration, lanes independent
                 int64_t X = 0;
                 double prod = 1.0;
                 for (int j = 0; j < nd;) {

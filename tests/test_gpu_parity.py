@@ -998,12 +998,15 @@ def test_full_size_rollout_vs_oracle(gpu, oracle, family, cls_name, n):
         oracle.set_threads(1)
 
 
-@pytest.mark.parametrize("mu_max,step_limit", [(9.0, 40), (14.0, 6), (60.0, 40), (200.0, 5)])
+@pytest.mark.parametrize("mu_max,step_limit", [(9.0, 40), (14.0, 6), (40.0, 13), (60.0, 40), (100.0, 40),
+                                             (200.0, 5), (400.0, 40)])
 def test_newsvendor_rollout_sampler_mixes(gpu, monkeypatch, mu_max, step_limit):
     """nv_roll_kernel's two stream waves (PTRS / multiplication branch) under
     every mix of rates -- all envs on the multiplication method, mixed, all
     PTRS -- and episodes shorter than a chunk give nv_run_kernel's outputs,
-    demands and state."""
+    demands and state.  The mu_max values put 1-64 envs of a workgroup on the
+    multiplication branch: the lane-group sampler at 16, 8 and 4 lanes per env
+    (up to 4 / 8 / 16 envs) and the one-lane fallback above 16."""
     import invsim
     n = 3000
     envs = []
