@@ -150,9 +150,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL ("nccl") over xGMI; INVSIM_BENCH_BACKEND=gloo rehearses the multi-rank
+    # path with several ranks on one GPU (RCCL refuses two ranks per device)
+    backend = os.environ.get("INVSIM_BENCH_BACKEND", "nccl")
     if world > 1:
+        local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -223,8 +230,10 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # collectives on device tensors over RCCL; gloo (rehearsal) reduces host copies
+    cdev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     total_steps = calls * steps_per_call  # env.step() calls over the batch
@@ -244,6 +253,7 @@ def main():
     stats = torch.stack([ret.sum(), (ret * ret).sum(),
                          torch.tensor(float(env2.num_envs), dtype=torch.float64, device=dev)])
     if world > 1:
+        stats = stats.to(cdev)
         dist.all_reduce(stats)
     stats = stats.cpu().tolist()
 
@@ -269,7 +279,8 @@ def main():
         "data": "synthetic (pre-generated random actions in HBM, seeds 0..N-1 per global env index)",
         "config": {"workload": wl["desc"], "envs_per_gpu": N, "global_envs": N * world,
                    "mode": args.mode + (f" K={K}" if K else ""), "autoreset": "next_step",
-                   "parallelism": f"dp{world} (env sharding, no data-path collective)"},
+                   "parallelism": f"dp{world} (env sharding, no data-path collective)",
+                   "backend": backend if world > 1 else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, calibrated)",

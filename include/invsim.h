@@ -248,7 +248,11 @@ int invsim_set_info_demand(invsim_handle *h, int64_t *demand);
  *   NetInvMgmt f64 [N][2 RL + 2 J + 2 E]: S[t, retail links], U[t+1, retail links],
  *                                    X[t+1, main nodes], R[t, reorder links], Y[t+1, reorder
  *                                    links], P[t, main nodes]  (network_management.py:436-619)
- *   Newsvendor: none (dim 0). */
+ *   Newsvendor f64 [N][5]:          revenue, purchase_cost, holding_cost,
+ *                                    lost_sales_penalty (newsvendor.py:149-170, 195-199)
+ *                                    and their NumPy-2 kinds packed as
+ *                                    k_rev + 3 k_pur + 9 k_hold + 27 k_pen
+ *                                    (0 Python float, 1 np.float32, 2 np.float64) */
 int invsim_info_record_dim(const invsim_handle *h, int32_t *dim);
 int invsim_set_info_record(invsim_handle *h, void *record);
 

@@ -625,6 +625,7 @@ int invsim_set_autoreset(invsim_handle *h, int32_t mode) {
 static int info_record_dim(const invsim_handle *h) {
     if (h->family == INVSIM_INVMGMT) return 2 * (h->im_m1 + 1) + 5;
     if (h->family == INVSIM_NETINVMGMT) return 2 * h->net.RL + 2 * h->net.J + 2 * h->net.E;
+    if (h->family == INVSIM_NEWSVENDOR) return 5;
     return 0;
 }
 

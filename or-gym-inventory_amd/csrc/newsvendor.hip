@@ -310,7 +310,8 @@ __device__ __forceinline__ float nv_ss(const NvParams &P, const PolicyIO &pol, i
 template <int LT>
 __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool valid, int sc, NvState<LT> &s,
                                              float action, float *orow, const double *lg_l, TableStage *ts,
-                                             double &reward, int64_t *dem, int64_t dpre = -1) {
+                                             double &reward, int64_t *dem, int64_t dpre = -1,
+                                             double *irec = nullptr) {
     const int64_t S = P.cm.Npad;
     const int L = (LT >= 0) ? LT : P.L;
     const int base = (L > 0) ? (int)((uint32_t)(sc + 1) % (uint32_t)L) : 0;  // slot of position 0
@@ -357,6 +358,14 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
     }
     reward = r.v;
     if (dem) dem[e] = d;
+    if (irec) {   // step info (:195-199): the cost components, values and NumPy-2 kinds
+        double *rr = irec + e * 5;
+        rr[0] = revenue.v;
+        rr[1] = purchase.v;
+        rr[2] = holding.v;
+        rr[3] = penalty.v;
+        rr[4] = (double)(revenue.k + 3 * purchase.k + 9 * holding.k + 27 * penalty.k);
+    }
     TPROBE(3);
     return sc + 1 >= P.step_limit;                                          // :190
 }
@@ -452,7 +461,8 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
                 if (valid && pol.act_out) out_store((float *)pol.act_out + oi, act);
             }
             const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, ts.dst, (ONE && TU) ? &ts : nullptr, r,
-                                             (valid && k == K - 1) ? P.cm.info_demand : nullptr);
+                                             (valid && k == K - 1) ? P.cm.info_demand : nullptr, -1,
+                                             (valid && k == K - 1) ? (double *)P.cm.info_rec : nullptr);
             if (POL) {
                 met[0] += r;                    // episode_reward += reward (benchmark_newsvendor.py:241)
                 met[1] += 1.0;
@@ -640,7 +650,8 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
     }
     double r;
     const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, lg_l, nullptr, r,
-                                     valid ? P.cm.info_demand : nullptr, dpre);
+                                     valid ? P.cm.info_demand : nullptr, dpre,
+                                     valid ? (double *)P.cm.info_rec : nullptr);
     if (valid) {
         out_store(io.rew + e, r);
         out_store(io.term + e, (uint8_t)0);
@@ -1011,7 +1022,8 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
             const int64_t d = dbuf[(cb * CH + kk) * WAVE + lane];
             double r;
             const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, lg_l, nullptr, r,
-                                             (valid && k == K - 1) ? P.cm.info_demand : nullptr, d);
+                                             (valid && k == K - 1) ? P.cm.info_demand : nullptr, d,
+                                             (valid && k == K - 1) ? (double *)P.cm.info_rec : nullptr);
             if (valid) {
                 out_store(io.rew + oi, r);
                 out_store(io.term + oi, (uint8_t)0);

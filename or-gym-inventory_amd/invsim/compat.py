@@ -17,7 +17,9 @@ unchanged:
 
 numpy in and out (the reference's dtypes); reward is a Python float.
 Stepping an InvManagement view past ``num_periods`` raises IndexError like the
-reference.  Not kept: NewsvendorEnv's per-step cost components in ``info``.
+reference.  NewsvendorEnv's per-step cost components come back with the
+NumPy-2 scalar type the reference's expression produces (Python float,
+np.float32 or np.float64).
 """
 import numpy as np
 import torch
@@ -175,6 +177,9 @@ class NewsvendorView(_View):
         self.period = self.step_count
         out = self._info()
         out["demand"] = int(info["demand"][0])
+        typ = (float, np.float32, np.float64)
+        for k in ("revenue", "purchase_cost", "holding_cost", "lost_sales_penalty"):   # newsvendor.py:195-199
+            out[k] = typ[int(info[k + "_kind"][0])](info[k][0].item())
         return obs[0].cpu().numpy(), float(r[0]), bool(te[0]), bool(tr[0]), out
 
 
@@ -184,9 +189,8 @@ def make(cls_name, device=None, **kwargs):
     import invsim
     cls = getattr(invsim, cls_name)
     fam = cls.family
-    vec_kw = dict(num_envs=1, device=device, autoreset_mode="disabled", record_demand=True)
-    if fam != _capi.INVSIM_NEWSVENDOR:
-        vec_kw["record_info"] = True
+    vec_kw = dict(num_envs=1, device=device, autoreset_mode="disabled", record_demand=True,
+                  record_info=True)
     vec = cls(**vec_kw, **kwargs)
     if fam == _capi.INVSIM_INVMGMT:
         return InvManagementView(vec)
