@@ -750,9 +750,8 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         }
         case INVSIM_NETINVMGMT: {
             StepIO<float, float> io{K, (const float *)actions, (float *)obs, reward, terminated, truncated, (float *)final_obs};
-            if (pol && !h->net_spec) return fail(h, INVSIM_EINVAL, "policy rollouts need the default or custom graph");
             e = h->net_spec ? net_spec_launch(h->net_spec, h->net, t_u, pol, io, h->la_valid, h->la_slot, s)
-                            : net_run_launch(h->net, t_u, io, s);
+                            : net_run_launch(h->net, t_u, pol, io, s);
             break;
         }
         default: return fail(h, INVSIM_EINVAL, "bad handle family");

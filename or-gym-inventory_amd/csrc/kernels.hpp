@@ -311,7 +311,9 @@ hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const PolicyI
                            const StepIO<float, float> &io, bool &ahead, int &slot, hipStream_t s);
 hipError_t net_commit_launch(const NetParams &p, int slot, hipStream_t s);
 hipError_t net_reset_launch(const NetParams &p, const uint8_t *mask, float *obs, hipStream_t s);
-hipError_t net_run_launch(const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s);
+// generic (table-walking) kernel; pol: CONSTANT policy rollouts, or null
+hipError_t net_run_launch(const NetParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
+                          hipStream_t s);
 size_t net_lds_bytes(const NetParams &p);
 
 }  // namespace invsim

@@ -200,9 +200,13 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, Pcg &
     return t + 1 >= P.T;
 }
 
-template <bool TU>
+// POL: closed-loop rollout (invsim_rollout_policy) with the CONSTANT agent
+// (ConstantOrderAgent, benchmark_NetInvMgmtBacklogEnv.py:119-135) on any graph:
+// every output optional, evaluate_agent metrics (as net_spec_kernel) summed
+// into pol.metrics in place.
+template <bool TU, bool POL>
 __global__ void __launch_bounds__(WAVE)
-net_run_kernel(NetParams P, int t_u, StepIO<float, float> io) {
+net_run_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) double net_lds[];
     const int lane = threadIdx.x;
     const int gl = lane & (LPE - 1);
@@ -236,7 +240,7 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io) {
             if (t >= P.T) {
                 if (P.cm.autoreset == AR_NEXT_STEP) {
                     net_reset_lds(P, s, leader ? trow : nullptr);
-                    if (leader) {
+                    if (leader && (!POL || io.rew)) {
                         io.rew[oi] = 0.0;
                         io.term[oi] = 0;
                         io.trunc[oi] = 0;
@@ -247,13 +251,32 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io) {
                 }
             } else {
                 double r;
-                tr = net_step_lds(P, e, gl, t, g, s, io.act + oi * P.E, trow, r,
+                tr = net_step_lds(P, e, gl, t, g, s, POL ? pol.cf : io.act + oi * P.E, trow, r,
                                   k == io.K - 1 ? P.cm.info_demand : nullptr,
                                   k == io.K - 1 ? (double *)P.cm.info_rec : nullptr);
-                if (leader) {
+                if (leader && (!POL || io.rew)) {
                     io.rew[oi] = r;
                     io.term[oi] = 0;
                     io.trunc[oi] = tr ? 1 : 0;
+                }
+                if (POL && leader) {
+                    if (pol.act_out)
+                        for (int q = 0; q < P.E; q++) ((float *)pol.act_out)[oi * P.E + q] = pol.cf[q];
+                    if (pol.metrics) {   // evaluate_agent metrics (benchmark_NetInvMgmtLostSalesEnv.py:264-300)
+                        double *met = pol.metrics + e * (5 + P.J);
+                        met[0] += r;                                   // episode_reward
+                        met[1] += 1.0;
+                        double m2 = met[2], m3 = met[3], m4 = met[4];
+                        for (int q = 0; q < P.RL; q++) {
+                            m2 += LV(s.Dd, q);                         // D[t, retail links]
+                            m3 += LV(s.Sr, q);                         // S[t, retail links]
+                            m4 += LV(s.U, q);                          // U[t+1, retail links]
+                        }
+                        met[2] = m2;
+                        met[3] = m3;
+                        met[4] = m4;
+                        for (int j = 0; j < P.J; j++) met[5 + j] += LV(s.X, j);   // X[t+1] per node
+                    }
                 }
                 t += 1;
             }
@@ -269,7 +292,7 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io) {
             }
             __syncthreads();
         }
-        store_tile(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+        if (!POL || io.obs) store_tile(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
         __syncthreads();
     }
     if (valid && leader) {
@@ -312,15 +335,22 @@ size_t net_lds_bytes(const NetParams &p) {
     return (size_t)scratch_rows(p.J, p.E, p.RL) * WAVE * sizeof(double) + (tile + 15) / 16 * 16;
 }
 
-hipError_t net_run_launch(const NetParams &p, int t_u, const StepIO<float, float> &io, hipStream_t s) {
+hipError_t net_run_launch(const NetParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
+                          hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = net_lds_bytes(p);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
-    if (t_u >= 0)
-        hipLaunchKernelGGL(net_run_kernel<true>, grid, block, lds, s, p, t_u, io);
-    else
-        hipLaunchKernelGGL(net_run_kernel<false>, grid, block, lds, s, p, t_u, io);
+    PolicyIO none{};
+    const PolicyIO &pv = pol ? *pol : none;
+    if (pol && pol->kind != POL_CONSTANT) return hipErrorInvalidValue;
+    if (t_u >= 0) {
+        if (pol) hipLaunchKernelGGL((net_run_kernel<true, true>), grid, block, lds, s, p, t_u, io, pv);
+        else hipLaunchKernelGGL((net_run_kernel<true, false>), grid, block, lds, s, p, t_u, io, pv);
+    } else {
+        if (pol) hipLaunchKernelGGL((net_run_kernel<false, true>), grid, block, lds, s, p, t_u, io, pv);
+        else hipLaunchKernelGGL((net_run_kernel<false, false>), grid, block, lds, s, p, t_u, io, pv);
+    }
     return hipGetLastError();
 }
 

@@ -106,6 +106,56 @@ def test_constant_order_net_vs_oracle(gpu, oracle, graph, frac):
     assert np.array_equal(met.cpu().numpy().view(np.uint64), e_sum.view(np.uint64))
 
 
+def _two_retailer_graph():
+    """A graph outside the compiled specialisations (generic kernel): the
+    default network with a second retailer off distributor 3."""
+    from invsim.topology import default_graph
+    g = default_graph()
+    g.add_nodes_from([9], I0=60, h=0.025)
+    g.add_edge(9, 0, p=2.5, b=0.2, dist_param={"lam": 7})
+    g.add_edge(3, 9, L=2, p=1.4, g=0.012)
+    return g
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["two_retailer", "forced_generic"])
+def test_constant_order_generic_kernel_vs_oracle(gpu, oracle, monkeypatch, which):
+    """ConstantOrderAgent rollouts on the table-walking kernel (any graph):
+    same actions, obs, rewards and evaluate_agent metrics as the oracle."""
+    import torch
+    import invsim
+    from invsim.topology import default_graph
+    n = 300
+    if which == "forced_generic":
+        monkeypatch.setenv("INVSIM_NET_GENERIC", "1")
+        g = default_graph()
+    else:
+        g = _two_retailer_graph()
+    env = invsim.NetInvMgmtBacklogEnv(n, device=gpu, graph=g, autoreset_mode="next_step", num_periods=12)
+    assert env.kernel_variant == 0
+    agent = invsim.ConstantOrderAgent(0.07)
+    a = agent.action(env)
+    orc = oracle.OracleNet(n, graph=g, num_periods=12)
+    orc.seed(range(44, 44 + n))
+    o0 = orc.reset()
+    env.reset(seed=44)
+    met = torch.zeros((n, invsim.policies.metrics_dim(env)), dtype=torch.float64, device=gpu)
+    out = env.rollout_policy(agent, 12, obs=True, actions=True, metrics=met)
+    e_rew, e_obs, e_sum = agents.run_net(orc, o0, 12, a)
+    assert np.array_equal(out["actions"].cpu().numpy(), np.broadcast_to(a, (12, n, len(a))))
+    assert np.array_equal(out["obs"].cpu().numpy().view(np.uint32), e_obs.view(np.uint32))
+    assert np.array_equal(out["reward"].cpu().numpy().view(np.uint64), e_rew.view(np.uint64))
+    assert np.array_equal(met.cpu().numpy().view(np.uint64), e_sum.view(np.uint64))
+    # metrics only (no per-step outputs), across the NEXT_STEP autoreset, chained
+    met2 = torch.zeros_like(met)
+    env.reset(seed=44)
+    env.rollout_policy(agent, 5, metrics=met2)
+    env.rollout_policy(agent, 7, metrics=met2)
+    assert torch.equal(met2, met)
+    out = env.rollout_policy(agent, 2, obs=True)
+    assert (out["reward"][0] == 0).all()             # the reset step of NEXT_STEP
+
+
 @pytest.mark.gpu
 def test_policy_rollout_chains_and_replays(gpu):
     """Metrics accumulate across launches; the actions the agent took, replayed
