@@ -513,9 +513,10 @@ def test_invmgmt_integers_buffer_is_state(gpu):
 
 
 def test_invmgmt_action_log_32bit_boundary(gpu, oracle):
-    """The action_log ring is 32-bit with a sentinel for values >= 2^32 - 1:
-    requested orders at and around the boundary round-trip exactly (obs window,
-    BaseStock pipeline) against the int64 oracle."""
+    """The action_log ring is 32-bit with a sentinel for values >= 2^32 - 1
+    (int64 side ring): requested orders at and around the boundary round-trip
+    exactly through single steps (two-wave kernel), fused rollouts
+    (register-window kernel) and the obs window, against the int64 oracle."""
     from invsim import InvManagementBacklogEnv
     n = 256
     env = InvManagementBacklogEnv(n, device=gpu, c=(2**40, 2**40, 2**40))
@@ -523,14 +524,29 @@ def test_invmgmt_action_log_32bit_boundary(gpu, oracle):
     orc.seed(range(9, 9 + n))
     orc.reset()
     env.reset(seed=9)
-    vals = np.array([0, 1, 2**31 - 1, 2**31, 2**32 - 2, 2**32 - 1, 2**32, 2**33 + 5, 2**40, 7], np.int64)
+    vals = np.array([0, 1, 2**15, 2**16 - 2, 2**16 - 1, 2**16, 2**16 + 1, 2**31, 2**32 - 1, 2**33 + 5,
+                     2**40, 7, 65534, 40000], np.int64)
     rng = np.random.default_rng(4)
-    for s in range(30):
-        a = vals[rng.integers(0, len(vals), size=(n, 3))]
-        o, r, te, tr, info = env.step(torch.from_numpy(a).to(gpu))
-        e_obs, e_rew, e_tr = orc.step(a)
-        assert np.array_equal(o.cpu().numpy(), e_obs), f"obs step {s}"
-        _assert_reward(r.cpu().numpy(), e_rew, f"step {s}")
+    s = 0
+    for phase in range(3):
+        a = vals[rng.integers(0, len(vals), size=(13, n, 3))]
+        if phase == 1:                                  # fused rollout (register windows)
+            o, r, te, tr = env.rollout(torch.from_numpy(a).to(gpu))
+            o, r = o.cpu().numpy(), r.cpu().numpy()
+        for k in range(13):
+            if phase != 1:
+                ok, rk, _, _, _ = env.step(torch.from_numpy(a[k]).to(gpu))
+                ok, rk = ok.cpu().numpy(), rk.cpu().numpy()
+            else:
+                ok, rk = o[k], r[k]
+            if s % 31 == 30:                            # NEXT_STEP autoreset step
+                e_obs = orc.reset()
+                assert np.array_equal(ok, e_obs), f"reset obs step {s}"
+            else:
+                e_obs, e_rew, e_tr = orc.step(a[k])
+                assert np.array_equal(ok, e_obs), f"obs step {s}"
+                _assert_reward(rk, e_rew, f"step {s}")
+            s += 1
 
 
 @pytest.mark.parametrize("cfg", [
