@@ -260,8 +260,11 @@ def main():
     B = wl["B_io"] + (wl["B_state_rollout"] / K if K else wl["B_state"])
     achieved = B * N * steps_per_call / (kern_ms_mean * 1e-3) / 1e9
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01", f"pmc_{args.workload}.json")
-    if os.path.exists(pmc) and args.mode == "step" and N == wl["n"]:
+    # the newest round's PMC summary (profiles/rNN/pmc_<workload>.json, tools/pmc_summary.py)
+    import glob
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", f"pmc_{args.workload}.json")))
+    pmc = pmcs[-1] if pmcs else ""
+    if pmc and args.mode == "step" and N == wl["n"]:
         rec = json.load(open(pmc))
         traffic, traffic_src = rec["hbm_bytes_per_launch"], os.path.relpath(pmc, ROOT)
     out = {
