@@ -555,6 +555,8 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
     const uint64_t *Acur = P.ahead + (int64_t)cur * 3 * S;
     uint64_t *Anxt = P.ahead + (int64_t)(cur ^ 1) * 3 * S;
     const int bid = (int)blockIdx.x;
+    TPROBE(0);
+    TPROBE_ID();
     if (HIT && bid < gla) {   // ---- lookahead workgroups
         // PRODUCE: two workgroups per 64 envs, one per branch of numpy's sampler
         // (bid even: PTRS for lam >= 10 and lam == 0; odd: the multiplication
@@ -591,7 +593,9 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
                 c.a2 = 2 * c.a;
                 c.k0 = 0;
                 c.nk = 0;
+                TPROBE(1);
                 const int64_t dn = nv_poisson_c(g, c, lg_l);
+                TPROBE(2);
                 if (valid) {
                     st_store(Anxt + e, g.hi);
                     st_store(Anxt + S + e, g.lo);
@@ -602,6 +606,8 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
             st_store(P.cm.rng.hi + e, g.hi);
             st_store(P.cm.rng.lo + e, g.lo);
         }
+        TWAIT();
+        TPROBE(5);
         return;
     }
     const int64_t e0 = (int64_t)(bid - (HIT ? gla : 0)) * EPW;
@@ -659,6 +665,7 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
     }
     wave_lds_sync();
     store_tile<TILE_IT>(nv_tile, io.obs + e0 * O, (int64_t)nvalid * O, lane);
+    TPROBE(4);
     if (!HIT) {   // PRODUCE (the host runs nv_run_kernel for !HIT && !PRODUCE)
         if (valid) {
             st_store((uint64_t *)Acur + e, st.g.hi);
@@ -671,6 +678,8 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
             st_store(Anxt + 2 * S + e, (uint64_t)dn);
         }
     }
+    TWAIT();
+    TPROBE(5);
 }
 
 __device__ __forceinline__ void nv_wg_sync() {

@@ -1,0 +1,6 @@
+set -o pipefail
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_policies.py -x -q --timeout 300 --timeout-method thread -m gpu -k "lookahead or golden or oracle or split" > gpurun_out/t_p2.log 2>&1 || { tail -40 gpurun_out/t_p2.log; exit 1; }
+tail -2 gpurun_out/t_p2.log
+A=or-gym-inventory_amd/invsim/_lib/ablate
+bash tools/ab.sh newsvendor step cur $A/libinvsim_OLD.so
+bash tools/ab.sh invmgmt_backlog step cur $A/libinvsim_OLD.so
