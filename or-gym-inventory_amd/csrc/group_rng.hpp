@@ -137,6 +137,112 @@ __device__ inline int64_t poisson_mult_grp(Pcg &g, double enlam) {
     }
 }
 
+// ---------------------------------------------------------------- PTRS with a compacted second round
+// One numpy PTRS draw per lane (one env per lane), for the demand lookahead
+// whose chain is the launch's tail.  The sequential loop runs until the
+// slowest of 64 lanes accepts (~3.5 candidates per wave against 1.15 per
+// lane).  Here every lane evaluates its first candidate; the ~13 % of lanes
+// that rejected are then packed into groups of CG = 4 lanes (up to 16 envs
+// per wave), lane j of a group evaluating candidate j of the env's stream
+// (LCG jump-ahead by 2j, group_rng.hpp), and the group takes the first
+// accepted one in stream order -- the same draw, value and final state as
+// numpy.  A group needs another round with probability ~0.13^4.  More than 16
+// rejecting lanes fall back to the sequential loop.
+constexpr int CG = 4;
+
+// this lane's jump constants for its group position (A_n, S_n, n = 2 (lane & 3)),
+// loaded early so the second round does not wait for them
+struct PtrsJumpLane {
+    uint64_t a_hi, a_lo, s_hi, s_lo;
+    __device__ __forceinline__ void load(int lane) {
+        const int n = 2 * (lane & (CG - 1));
+        a_hi = c_jump.a_hi[n];
+        a_lo = c_jump.a_lo[n];
+        s_hi = c_jump.s_hi[n];
+        s_lo = c_jump.s_lo[n];
+    }
+};
+
+// one PTRS candidate (numpy random_poisson_ptrs loop body) from two uniforms of
+// g; rhs(k, c) = -lam + k log lam - loggam(k + 1)
+template <class Rhs>
+__device__ __forceinline__ bool ptrs_candidate(Pcg &g, const PtrsConst &c, Rhs rhs, int64_t &k) {
+    const double U = g.next_double() - 0.5;
+    const double V = g.next_double();
+    const double us = 0.5 - fabs(U);
+    k = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+    if ((us >= 0.07) && (V <= c.vr)) return true;
+    if ((k < 0) || ((us < 0.013) && (V > us))) return false;
+    return ptrs_log_accept(c, V, us, rhs(k, c));
+}
+
+// PTRS draw of the lane's env (c.lam >= 10 for every lane that calls it with
+// `live`; lanes with !live take part in the wave's shuffles only).  For a
+// per-env rate, `shfl_c` moves the constants to the group (identity when they
+// are wave-uniform).
+template <class Rhs, class ShflC>
+__device__ __forceinline__ int64_t np_poisson_ptrs_compact(Pcg &g, const PtrsConst &c, Rhs rhs, bool live,
+                                                           const PtrsJumpLane &jt, ShflC shfl_c) {
+    const int lane = (int)(threadIdx.x & 63);
+    int64_t k = 0;
+    bool acc = !live || ptrs_candidate(g, c, rhs, k);
+    const uint64_t rem = (uint64_t)__ballot(!acc);
+    const int nr = __popcll(rem);
+    if (nr == 0) return k;
+    if (nr > 64 / CG) {                                   // sequential fallback
+        while (!acc) acc = ptrs_candidate(g, c, rhs, k);
+        return k;
+    }
+    // group r (lanes 4r .. 4r + 3) works for the r-th rejecting lane
+    const int grp = lane / CG, jl = lane & (CG - 1), gbase = grp * CG;
+    uint64_t x = rem;
+    for (int i = 0; i < grp && x; i++) x &= x - 1;
+    const bool act = grp < nr;
+    const int src = act ? (int)__builtin_ctzll(x) : lane;
+    Pcg s;                                                // the env's state after its first candidate
+    s.hi = shfl_u64(g.hi, src);
+    s.lo = shfl_u64(g.lo, src);
+    s.inc_hi = shfl_u64(g.inc_hi, src);
+    s.inc_lo = shfl_u64(g.inc_lo, src);
+    const PtrsConst cc = shfl_c(c, src);
+    uint64_t sih, sil;                                    // S_n * inc
+    mul128(jt.s_hi, jt.s_lo, s.inc_hi, s.inc_lo, sih, sil);
+    bool done = !act;
+    int64_t kk = 0;
+    while (__ballot(!done)) {
+        Pcg t = s;                                        // candidate jl: LCG steps 2 jl + 1, 2 jl + 2
+        uint64_t ah, al;
+        mul128(jt.a_hi, jt.a_lo, s.hi, s.lo, ah, al);
+        t.lo = al + sil;
+        t.hi = ah + sih + (t.lo < al ? 1ULL : 0ULL);
+        int64_t kj = 0;
+        const bool aj = !done && ptrs_candidate(t, cc, rhs, kj);
+        const unsigned gm = (unsigned)((uint64_t)__ballot(aj) >> gbase) & ((1u << CG) - 1u);
+        const int win = gbase + (gm ? __builtin_ctz(gm) : CG - 1);   // first accepted, or the last candidate
+        const uint64_t nh = shfl_u64(t.hi, win), nl = shfl_u64(t.lo, win);
+        const int64_t kw = (int64_t)shfl_u64((uint64_t)kj, win);
+        if (!done) {
+            s.hi = nh;
+            s.lo = nl;
+            if (gm) {
+                kk = kw;
+                done = true;
+            }
+        }
+    }
+    // the result and the advanced generator back to the rejecting lane (group rank)
+    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(rem >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rem, 0u));
+    const int back = (!acc) ? rank * CG : lane;
+    const uint64_t bh = shfl_u64(s.hi, back), bl = shfl_u64(s.lo, back);
+    const int64_t bk = (int64_t)shfl_u64((uint64_t)kk, back);
+    if (!acc) {
+        g.hi = bh;
+        g.lo = bl;
+        k = bk;
+    }
+    return k;
+}
+
 // numpy random_poisson with fixed-lam constants (host libm) and optional RHS table
 __device__ __forceinline__ int64_t np_poisson_grp(Pcg &g, const PtrsConst &c, const double *rhs) {
     if (c.lam >= 10) return poisson_ptrs_grp(g, c, rhs);

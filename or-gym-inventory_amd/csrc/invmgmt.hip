@@ -643,9 +643,19 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         g.inc_hi = P.cm.rng.inc_hi[ee];
         g.inc_lo = P.cm.rng.inc_lo[ee];
         uint64_t u32 = NPD ? Acur[3 * S + ee] : 0;
+        PtrsJumpLane jt;
+        jt.load((int)(threadIdx.x & (WAVE - 1)));
         ts.flush((int)(threadIdx.x & (WAVE - 1)));   // each wave writes the whole (identical) table
         // slot cur keeps this state: the committed one once the slots flip
-        const int64_t dn = draw(g, u32);
+        int64_t dn;
+#ifndef INVSIM_ABL_NO_POISSON
+        if (!NPD && P.dist == 1 && P.pc.lam >= 10)   // PTRS with a compacted second round
+            dn = np_poisson_ptrs_compact(
+                g, P.pc, [&](int64_t k, const PtrsConst &c) { return ptrs_rhs(c, rhs_l, k); }, true, jt,
+                [](const PtrsConst &c, int) { return c; });
+        else
+#endif
+            dn = draw(g, u32);
         if (valid) {
             st_store(Anxt + e, g.hi);
             st_store(Anxt + S + e, g.lo);

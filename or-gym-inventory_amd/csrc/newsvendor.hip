@@ -580,27 +580,51 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
                 ts.flush(lane);
             }
             const bool mine = mult_wg == (mu < 10 && mu != 0);
-            if (mine) {
-                // the chain's constants (nv_rate_const(mu), stored by its first launch)
-                PtrsConst c;
-                c.lam = mu;
-                c.a = P.pcon[el];
-                c.b = P.pcon[S + el];
-                c.vr = P.pcon[2 * S + el];
-                c.loglam = P.pcon[3 * S + el];
-                c.log_invalpha = P.pcon[4 * S + el];
-                c.enlam = P.pcon[5 * S + el];
-                c.a2 = 2 * c.a;
-                c.k0 = 0;
-                c.nk = 0;
-                TPROBE(1);
-                const int64_t dn = nv_poisson_c(g, c, lg_l);
-                TPROBE(2);
-                if (valid) {
-                    st_store(Anxt + e, g.hi);
-                    st_store(Anxt + S + e, g.lo);
-                    st_store(Anxt + 2 * S + e, (uint64_t)dn);
-                }
+            // the chain's constants (nv_rate_const(mu), stored by its first launch)
+            PtrsConst c;
+            c.lam = mu;
+            c.a = P.pcon[el];
+            c.b = P.pcon[S + el];
+            c.vr = P.pcon[2 * S + el];
+            c.loglam = P.pcon[3 * S + el];
+            c.log_invalpha = P.pcon[4 * S + el];
+            c.enlam = P.pcon[5 * S + el];
+            c.a2 = 2 * c.a;
+            c.k0 = 0;
+            c.nk = 0;
+            TPROBE(1);
+            int64_t dn = 0;
+            if (!mult_wg) {   // PTRS (lam >= 10) with a compacted second round (group_rng.hpp)
+                PtrsJumpLane jt;
+                jt.load(lane);
+                const bool live = mine && c.lam >= 10;
+                dn = np_poisson_ptrs_compact(
+                    g, c,
+                    [&](int64_t k, const PtrsConst &cc) {   // as np_poisson_ptrs_lg
+                        return (k < RHS_LDS_MAX) ? (-cc.lam + (double)k * cc.loglam) - lg_l[k < RHS_LDS_MAX ? k : 0]
+                                                 : -cc.lam + (double)k * cc.loglam - np_loggam((double)(k + 1));
+                    },
+                    live, jt,
+                    [](const PtrsConst &cc, int src) {
+                        PtrsConst r = cc;
+                        r.lam = __shfl(cc.lam, src);
+                        r.a2 = __shfl(cc.a2, src);
+                        r.b = __shfl(cc.b, src);
+                        r.vr = __shfl(cc.vr, src);
+                        r.loglam = __shfl(cc.loglam, src);
+                        r.log_invalpha = __shfl(cc.log_invalpha, src);
+                        r.a = __shfl(cc.a, src);
+                        return r;
+                    });
+                if (mine && !live) dn = nv_poisson_c(g, c, lg_l);   // lam == 0 or NaN
+            } else if (mine) {
+                dn = nv_poisson_c(g, c, lg_l);
+            }
+            TPROBE(2);
+            if (mine && valid) {
+                st_store(Anxt + e, g.hi);
+                st_store(Anxt + S + e, g.lo);
+                st_store(Anxt + 2 * S + e, (uint64_t)dn);
             }
         } else if (valid) {
             st_store(P.cm.rng.hi + e, g.hi);
