@@ -496,9 +496,21 @@ net_step1_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
         g.lo = Acur[S + el];
         g.inc_hi = P.cm.rng.inc_hi[el];
         g.inc_lo = P.cm.rng.inc_lo[el];
+        PtrsJumpLane jt;
+        jt.load(lane);
         flush(tv);
         double Dd[RL];
-        spec_demand<G>(g, pc, rhs_l, Dd);
+#pragma unroll
+        for (int r = 0; r < RL; r++) {   // spec_demand, PTRS with a compacted second round
+            const double *rt = rhs_l + r * RHS_LDS_MAX;
+            const int64_t pd =
+                pc[r].lam >= 10
+                    ? np_poisson_ptrs_compact(
+                          g, pc[r], [&](int64_t k, const PtrsConst &c) { return ptrs_rhs(c, rt, k); }, true, jt,
+                          [](const PtrsConst &c, int) { return c; })
+                    : np_poisson(g, pc[r], rt);
+            Dd[r] = (double)(pd > 0 ? pd : 0);
+        }
         if (valid) {
             st_store(Anxt + e, g.hi);
             st_store(Anxt + S + e, g.lo);
@@ -646,9 +658,21 @@ net_step2_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
         g.lo = Acur[S + el];
         g.inc_hi = P.cm.rng.inc_hi[el];
         g.inc_lo = P.cm.rng.inc_lo[el];
+        PtrsJumpLane jt;
+        jt.load(lane);
         flush(tv);
         double Dd[RL];
-        spec_demand<G>(g, pc, rhs_l, Dd);
+#pragma unroll
+        for (int r = 0; r < RL; r++) {   // spec_demand, PTRS with a compacted second round
+            const double *rt = rhs_l + r * RHS_LDS_MAX;
+            const int64_t pd =
+                pc[r].lam >= 10
+                    ? np_poisson_ptrs_compact(
+                          g, pc[r], [&](int64_t k, const PtrsConst &c) { return ptrs_rhs(c, rt, k); }, true, jt,
+                          [](const PtrsConst &c, int) { return c; })
+                    : np_poisson(g, pc[r], rt);
+            Dd[r] = (double)(pd > 0 ? pd : 0);
+        }
         if (valid) {
             st_store(Anxt + e, g.hi);
             st_store(Anxt + S + e, g.lo);
