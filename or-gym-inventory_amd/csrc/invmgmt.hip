@@ -632,6 +632,8 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         return x < 0 ? 0 : x;
     };
     const int bid = (int)blockIdx.x;
+    TPROBE(0);
+    TPROBE_ID();
     if (AHEAD && bid >= la0 && bid < la0 + gla) {   // ---- lookahead workgroup: 128 envs, one per lane
         const int64_t e = (int64_t)(bid - la0) * (2 * WAVE) + threadIdx.x;
         const bool valid = e < N;
@@ -646,6 +648,7 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         PtrsJumpLane jt;
         jt.load((int)(threadIdx.x & (WAVE - 1)));
         ts.flush((int)(threadIdx.x & (WAVE - 1)));   // each wave writes the whole (identical) table
+        TPROBE(1);
         // slot cur keeps this state: the committed one once the slots flip
         int64_t dn;
 #ifndef INVSIM_ABL_NO_POISSON
@@ -656,12 +659,15 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         else
 #endif
             dn = draw(g, u32);
+        TPROBE(2);
         if (valid) {
             st_store(Anxt + e, g.hi);
             st_store(Anxt + S + e, g.lo);
             st_store(Anxt + 2 * S + e, (uint64_t)dn);
             if (NPD) st_store(Anxt + 3 * S + e, u32);
         }
+        TWAIT();
+        TPROBE(5);
         return;
     }
     const int lane = threadIdx.x & (WAVE - 1);
@@ -761,9 +767,12 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
                 if (NPD) st_store(Anxt + 3 * S + e, u32);
             }
         }
+        TWAIT();
+        TPROBE(5);   // the window wave's exit
         return;
     }
     // ---- dynamics wave
+    TPROBE_AT(3, WAVE);
     const double apow = P.alpha_pow[t];
     const int64_t *arow = io.act + (valid ? e : N - 1) * M1;
     int64_t req[M1], arr[M1], I[M1], B[M1 + 1];
@@ -869,6 +878,8 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
 #pragma unroll
         for (int q = 0; q <= M1; q++) st_store(P.B + q * S + e, U[q]);   // :307-312
     }
+    TWAIT();
+    TPROBE_AT(4, WAVE);   // the dynamics wave's exit (probe 3: its entry)
 }
 
 // K-step lock-step rollout (invsim_rollout, NEXT_STEP or DISABLED autoreset,

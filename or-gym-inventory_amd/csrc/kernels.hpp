@@ -32,8 +32,14 @@ constexpr int TB_WAVES = 4096, TB_PROBES = 8;   // probe 7: hardware ids
                 ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |                 \
                 (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                           \
     } while (0)
+#define TPROBE_AT(i, tid)                                                                      \
+    do {                                                                                       \
+        if (threadIdx.x == (tid) && blockIdx.x < TB_WAVES)                                     \
+            g_tbuf[blockIdx.x * TB_PROBES + (i)] = __builtin_amdgcn_s_memrealtime();           \
+    } while (0)
 #define TWAIT() __builtin_amdgcn_s_waitcnt(0)
 #else
+#define TPROBE_AT(i, tid) do {} while (0)
 #define TPROBE(i) do {} while (0)
 #define TPROBE_ID() do {} while (0)
 #define TWAIT() do {} while (0)
