@@ -13,6 +13,8 @@
 #include "../../include/invsim.h"
 #include "kernels.hpp"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 using namespace invsim;
 
 namespace {
@@ -61,6 +63,14 @@ struct invsim_handle {
 };
 
 namespace {
+
+// roctx range around an ABI call (SURVEY §5 tracing: step / rollout / reset
+// show up as named ranges under `rocprofv3 --marker-trace`; a no-op call when
+// no profiler is attached)
+struct TraceRange {
+    explicit TraceRange(const char *name) { roctxRangePushA(name); }
+    ~TraceRange() { roctxRangePop(); }
+};
 
 struct DeviceGuard {
     int prev = -1;
@@ -662,6 +672,7 @@ static int commit_rng(invsim_handle *h, hipStream_t s) {
 
 int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int64_t first,
                       const uint8_t *mask, void *stream) {
+    TraceRange tr_("invsim_seed_range");
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (first < 0) return fail(h, INVSIM_EINVAL, "first_index must be >= 0");
     DeviceGuard g(h->device);
@@ -674,6 +685,7 @@ int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int6
 
 int invsim_seed_words(invsim_handle *h, const uint32_t *words, const int32_t *nwords,
                       const uint8_t *mask, void *stream) {
+    TraceRange tr_("invsim_seed_words");
     if (!h || (!words && h->N) || (!nwords && h->N)) return fail(h, INVSIM_EINVAL, "null argument");
     DeviceGuard g(h->device);
     int rc = commit_rng(h, (hipStream_t)stream);
@@ -691,6 +703,7 @@ static int materialize_period(invsim_handle *h, hipStream_t s) {
 }
 
 int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream) {
+    TraceRange tr_("invsim_reset");
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
@@ -783,6 +796,7 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
 
 int invsim_step(invsim_handle *h, const void *actions, void *obs, double *reward, uint8_t *terminated,
                 uint8_t *truncated, void *final_obs, void *stream) {
+    TraceRange tr_("invsim_step");
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (h->N && (!actions || !obs || !reward || !terminated || !truncated))
         return fail(h, INVSIM_EINVAL, "null output/input buffer");
@@ -793,6 +807,7 @@ int invsim_step(invsim_handle *h, const void *actions, void *obs, double *reward
 
 int invsim_rollout(invsim_handle *h, int32_t K, const void *actions, void *obs, double *reward,
                    uint8_t *terminated, uint8_t *truncated, void *stream) {
+    TraceRange tr_("invsim_rollout");
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (K < 0) return fail(h, INVSIM_EINVAL, "K must be >= 0");
     if (K == 0) return INVSIM_OK;
@@ -821,6 +836,7 @@ int invsim_metrics_dim(const invsim_handle *h, int32_t *dim) {
 
 int invsim_rollout_policy(invsim_handle *h, int32_t K, const invsim_policy *policy, void *obs, double *reward,
                           uint8_t *terminated, uint8_t *truncated, void *actions, double *metrics, void *stream) {
+    TraceRange tr_("invsim_rollout_policy");
     if (!h || !policy) return fail(h, INVSIM_EINVAL, "null argument");
     if (K < 0) return fail(h, INVSIM_EINVAL, "K must be >= 0");
     if (K == 0) return INVSIM_OK;
@@ -912,6 +928,7 @@ int invsim_state_field(const invsim_handle *h, int32_t idx, char name[32], int64
 }
 
 int invsim_get_state(invsim_handle *h, void *dst, void *stream) {
+    TraceRange tr_("invsim_get_state");
     if (!h || !dst) return fail(h, INVSIM_EINVAL, "null argument");
     DeviceGuard g(h->device);
     int rc = materialize_period(h, (hipStream_t)stream);  // the blob carries per-env periods
@@ -923,6 +940,7 @@ int invsim_get_state(invsim_handle *h, void *dst, void *stream) {
 }
 
 int invsim_set_state(invsim_handle *h, const void *src, void *stream) {
+    TraceRange tr_("invsim_set_state");
     if (!h || !src) return fail(h, INVSIM_EINVAL, "null argument");
     DeviceGuard g(h->device);
     hipError_t e = hipMemcpyAsync(h->arena, src, (size_t)h->arena_bytes, hipMemcpyDeviceToDevice,
