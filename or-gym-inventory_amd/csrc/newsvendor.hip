@@ -580,15 +580,19 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
                 ts.flush(lane);
             }
             const bool mine = mult_wg == (mu < 10 && mu != 0);
-            // the chain's constants (nv_rate_const(mu), stored by its first launch)
+            // the chain's constants (nv_rate_const(mu), stored by its first launch),
+            // read only by the lanes whose env this workgroup draws for
             PtrsConst c;
             c.lam = mu;
-            c.a = P.pcon[el];
-            c.b = P.pcon[S + el];
-            c.vr = P.pcon[2 * S + el];
-            c.loglam = P.pcon[3 * S + el];
-            c.log_invalpha = P.pcon[4 * S + el];
-            c.enlam = P.pcon[5 * S + el];
+            c.a = c.b = c.vr = c.loglam = c.log_invalpha = c.enlam = 0.0;
+            if (mine) {
+                c.a = P.pcon[el];
+                c.b = P.pcon[S + el];
+                c.vr = P.pcon[2 * S + el];
+                c.loglam = P.pcon[3 * S + el];
+                c.log_invalpha = P.pcon[4 * S + el];
+                c.enlam = P.pcon[5 * S + el];
+            }
             c.a2 = 2 * c.a;
             c.k0 = 0;
             c.nk = 0;
