@@ -173,24 +173,87 @@ def summarize(family, m, main_nodes=None):
     return rows
 
 
-def evaluate_agent(agent, env_cls, env_config=None, n_episodes=100, seed_offset=0, device=None):
+def _gather_rows(met, n_episodes, world, rank, group):
+    """All ranks' per-episode metric rows, in global episode order (one
+    all_gather of a padded [ceil(n / world), M] block; RCCL for device tensors
+    with the nccl backend, host tensors with gloo)."""
+    import torch.distributed as dist
+    from .distributed import shard_range
+    nmax = -(-n_episodes // world)
+    dev = met.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    pad = torch.zeros((nmax, met.shape[1]), dtype=torch.float64, device=dev)
+    pad[:met.shape[0]] = met.to(dev)
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return torch.cat([parts[r][:shard_range(n_episodes, r, world)[1]] for r in range(world)]).cpu()
+
+
+def evaluate_agent(agent, env_cls, env_config=None, n_episodes=100, seed_offset=0, device=None, group=None):
     """Batched evaluate_agent: episode i = env i seeded seed_offset + i, one
     full episode under ``agent`` in one kernel launch.  Returns a dict of
-    per-episode columns (the reference's summary DataFrame columns)."""
-    env = env_cls(num_envs=n_episodes, device=device, autoreset_mode="disabled", **(env_config or {}))
+    per-episode columns (the reference's summary DataFrame columns).
+
+    Under torch.distributed (one process per GPU) the episodes are sharded by
+    global index over the ranks of ``group`` (rank r runs episodes
+    [offset_r, offset_r + n_r), seeded by global index as above) and every
+    rank gets all episodes' columns, gathered in one collective; Time is the
+    slowest rank's time per episode."""
+    import torch.distributed as dist
+    from .distributed import shard_range
+    on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if on else 1
+    rank = dist.get_rank(group) if on else 0
+    off, n_loc = shard_range(n_episodes, rank, world)
+    env = env_cls(num_envs=max(n_loc, 1), device=device, autoreset_mode="disabled", global_offset=off,
+                  **(env_config or {}))
     try:
         env.reset(seed=seed_offset)
         M = metrics_dim(env)
-        met = torch.zeros((n_episodes, M), dtype=torch.float64, device=env.device)
+        met = torch.zeros((env.num_envs, M), dtype=torch.float64, device=env.device)
         torch.cuda.synchronize(env.device)
         t0 = time.perf_counter()
         rollout_policy(env, agent, env._horizon(), obs=False, rewards=False, metrics=met)
         torch.cuda.synchronize(env.device)
         dt = time.perf_counter() - t0
-        cols = summarize(env.family, met.cpu().numpy())
-        n = n_episodes
-        out = {"Agent": [agent.name] * n, "Episode": np.arange(1, n + 1), **cols,
-               "Time": np.full(n, dt / max(n, 1)), "Seed": seed_offset + np.arange(n), "Error": [None] * n}
-        return out
+        met = met[:n_loc]
+        family = env.family
     finally:
         env.close()
+    if world > 1:
+        met = _gather_rows(met, n_episodes, world, rank, group)
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+            else torch.device("cpu")
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        dt = float(t.item())
+    cols = summarize(family, met.cpu().numpy())
+    n = n_episodes
+    return {"Agent": [agent.name] * n, "Episode": np.arange(1, n + 1), **cols,
+            "Time": np.full(n, dt / max(n, 1)), "Seed": seed_offset + np.arange(n), "Error": [None] * n}
+
+
+def summary_table(results):
+    """The reference's benchmark summary (process_and_report_results,
+    benchmark_InvManagementBacklogEnv.py:474-516; the NetInvMgmt scripts'
+    :333-353 are the same): per agent the mean / median / std / min / max
+    episode reward, mean service level, stockout and ending inventory, time per
+    episode, and episode counts, sorted by AvgReward.  ``results``: a list of
+    evaluate_agent outputs.  Returns a pandas DataFrame indexed by Agent."""
+    import pandas as pd
+    raw = pd.concat([pd.DataFrame(r) for r in results], ignore_index=True)
+    for c in ("AvgServiceLevel", "TotalStockoutQty", "AvgEndingInv"):
+        if c not in raw:
+            raw[c] = np.nan
+    summary = raw.dropna(subset=["TotalReward"]).groupby("Agent").agg(
+        AvgReward=("TotalReward", "mean"), MedianReward=("TotalReward", "median"),
+        StdReward=("TotalReward", "std"), MinReward=("TotalReward", "min"), MaxReward=("TotalReward", "max"),
+        AvgServiceLevel=("AvgServiceLevel", "mean"), AvgStockoutQty=("TotalStockoutQty", "mean"),
+        AvgEndInv=("AvgEndingInv", "mean"), AvgTimePerEp=("Time", "mean"),
+        SuccessfulEpisodes=("Episode", "count"))
+    summary["TrainingTime(s)"] = 0.0                    # heuristic agents do not train
+    summary["EpisodesAttempted"] = raw.groupby("Agent")["Episode"].count()
+    summary["SuccessRate(%)"] = (summary["SuccessfulEpisodes"] / summary["EpisodesAttempted"]) * 100
+    summary = summary.sort_values(by="AvgReward", ascending=False)
+    return summary[["AvgReward", "MedianReward", "StdReward", "MinReward", "MaxReward", "AvgServiceLevel",
+                    "AvgStockoutQty", "AvgEndInv", "AvgTimePerEp", "TrainingTime(s)", "SuccessfulEpisodes",
+                    "EpisodesAttempted", "SuccessRate(%)"]]

@@ -384,3 +384,33 @@ def test_classic_nv_across_autoresets(gpu, oracle):
     assert np.array_equal(obs[12], o1) and np.array_equal(obs[13:], ob2)
     rew = out["reward"].cpu().numpy()
     assert np.array_equal(rew[:12], r1) and np.array_equal(rew[13:], r2) and not rew[12].any()
+
+
+def test_summary_table_matches_reference_aggregation():
+    """summary_table restates process_and_report_results
+    (benchmark_InvManagementBacklogEnv.py:474-516): per agent mean / median /
+    sample std / min / max of TotalReward, means of the per-episode metrics,
+    counts and success rate, sorted by AvgReward."""
+    from invsim.policies import summary_table
+    rng = np.random.default_rng(3)
+
+    def res(name, n):
+        return {"Agent": [name] * n, "Episode": np.arange(1, n + 1), "TotalReward": rng.normal(size=n),
+                "Steps": np.full(n, 30), "AvgServiceLevel": rng.uniform(size=n),
+                "TotalStockoutQty": rng.uniform(size=n) * 9, "AvgEndingInv": rng.uniform(size=n) * 50,
+                "Time": np.full(n, 1e-4), "Seed": np.arange(n), "Error": [None] * n}
+    rs = [res("BaseStock", 7), res("Constant", 5)]
+    t = summary_table(rs)
+    for r in rs:
+        row = t.loc[r["Agent"][0]]
+        x = r["TotalReward"]
+        assert row["AvgReward"] == pytest.approx(x.mean())
+        assert row["MedianReward"] == pytest.approx(np.median(x))
+        assert row["StdReward"] == pytest.approx(x.std(ddof=1))
+        assert row["MinReward"] == x.min() and row["MaxReward"] == x.max()
+        assert row["AvgServiceLevel"] == pytest.approx(r["AvgServiceLevel"].mean())
+        assert row["AvgStockoutQty"] == pytest.approx(r["TotalStockoutQty"].mean())
+        assert row["AvgEndInv"] == pytest.approx(r["AvgEndingInv"].mean())
+        assert row["SuccessfulEpisodes"] == len(x) == row["EpisodesAttempted"]
+        assert row["SuccessRate(%)"] == 100.0
+    assert list(t.index) == sorted(t.index, key=lambda a: -t.loc[a, "AvgReward"])
