@@ -180,14 +180,20 @@ __device__ __forceinline__ bool ptrs_candidate(Pcg &g, const PtrsConst &c, Rhs r
 // `live`; lanes with !live take part in the wave's shuffles only).  For a
 // per-env rate, `shfl_c` moves the constants to the group (identity when they
 // are wave-uniform).
-template <class Rhs, class ShflC>
+struct NoProbe {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <class Rhs, class ShflC, class Probe = NoProbe>
 __device__ __forceinline__ int64_t np_poisson_ptrs_compact(Pcg &g, const PtrsConst &c, Rhs rhs, bool live,
-                                                           const PtrsJumpLane &jt, ShflC shfl_c) {
+                                                           const PtrsJumpLane &jt, ShflC shfl_c,
+                                                           Probe probe = Probe()) {
     const int lane = (int)(threadIdx.x & 63);
     int64_t k = 0;
     bool acc = !live || ptrs_candidate(g, c, rhs, k);
     const uint64_t rem = (uint64_t)__ballot(!acc);
     const int nr = __popcll(rem);
+    probe(3);    // profiling hook (TIMING build): first candidate evaluated
     if (nr == 0) return k;
     if (nr > 64 / CG) {                                   // sequential fallback
         while (!acc) acc = ptrs_candidate(g, c, rhs, k);
@@ -195,10 +201,16 @@ __device__ __forceinline__ int64_t np_poisson_ptrs_compact(Pcg &g, const PtrsCon
     }
     // group r (lanes 4r .. 4r + 3) works for the r-th rejecting lane
     const int grp = lane / CG, jl = lane & (CG - 1), gbase = grp * CG;
-    uint64_t x = rem;
-    for (int i = 0; i < grp && x; i++) x &= x - 1;
+    int src = lane;                                       // the grp-th set bit of rem: a wave-uniform
+    {                                                     // scalar walk over rem's <= 16 bits
+        uint64_t x = rem;
+        for (int r = 0; r < nr; r++) {
+            const int pos = (int)__builtin_ctzll(x);
+            x &= x - 1;
+            if (r == grp) src = pos;
+        }
+    }
     const bool act = grp < nr;
-    const int src = act ? (int)__builtin_ctzll(x) : lane;
     Pcg s;                                                // the env's state after its first candidate
     s.hi = shfl_u64(g.hi, src);
     s.lo = shfl_u64(g.lo, src);
@@ -207,6 +219,7 @@ __device__ __forceinline__ int64_t np_poisson_ptrs_compact(Pcg &g, const PtrsCon
     const PtrsConst cc = shfl_c(c, src);
     uint64_t sih, sil;                                    // S_n * inc
     mul128(jt.s_hi, jt.s_lo, s.inc_hi, s.inc_lo, sih, sil);
+    probe(4);    // profiling hook: groups formed
     bool done = !act;
     int64_t kk = 0;
     while (__ballot(!done)) {

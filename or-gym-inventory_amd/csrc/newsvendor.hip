@@ -619,7 +619,8 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
                         r.log_invalpha = __shfl(cc.log_invalpha, src);
                         r.a = __shfl(cc.a, src);
                         return r;
-                    });
+                    },
+                    [&](int i) { TPROBE_AT(i, 0); });
                 if (mine && !live) dn = nv_poisson_c(g, c, lg_l);   // lam == 0 or NaN
             } else if (mine) {
                 dn = nv_poisson_c(g, c, lg_l);

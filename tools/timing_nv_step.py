@@ -48,6 +48,15 @@ def main():
             if len(live):
                 print("  entry->loaded  " + fmt(live[:, 1] - live[:, 0]))
                 print("  draw           " + fmt(live[:, 2] - live[:, 1]))
+                if name.endswith("PTRS"):
+                    c = live[(live[:, 3] > live[:, 1]) & (live[:, 3] < live[:, 2])]
+                    print(f"  (compaction probes in {len(c)} waves)")
+                    if len(c):
+                        print("  round 1        " + fmt(c[:, 3] - c[:, 1]))
+                        g = c[(c[:, 4] > c[:, 3]) & (c[:, 4] < c[:, 2])]
+                        if len(g):
+                            print("  group setup    " + fmt(g[:, 4] - g[:, 3]))
+                            print("  group rounds   " + fmt(g[:, 2] - g[:, 4]))
                 print("  drawn->exit    " + fmt(live[:, 5] - live[:, 2]))
         else:
             print("  entry->p1      " + fmt(sel[:, 1] - sel[:, 0]))
