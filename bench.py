@@ -210,17 +210,22 @@ def main():
 
     calls = max(1, args.steps // steps_per_call)
     warm = max(1, args.warmup // steps_per_call)
+    # HIP events on the stream the kernels run on, around the timed region:
+    # launches are back to back there, so (end - start) / calls is the mean
+    # kernel duration (+ inter-kernel gaps, ~0 on a saturated queue).  torch
+    # creates the HIP event at its first record: record both once here so the
+    # creation stays out of the timed region (~10 us of wall time per region,
+    # tools/sync_overhead.py)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
     for i in range(warm):
         one(i)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    # HIP events on the stream the kernels run on, around the timed region:
-    # launches are back to back there, so (end - start) / calls is the mean
-    # kernel duration (+ inter-kernel gaps, ~0 on a saturated queue)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
     for i in range(calls):

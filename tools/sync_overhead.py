@@ -12,6 +12,13 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "or-gym-inventory_amd"))
 
+if "--spin" in sys.argv:
+    # hipDeviceScheduleSpin (= 1) before the first context: host waits spin
+    # instead of yielding / blocking on an interrupt
+    import ctypes
+    _hip = ctypes.CDLL("libamdhip64.so")
+    print("hipSetDeviceFlags(spin) ->", _hip.hipSetDeviceFlags(ctypes.c_uint(1)), flush=True)
+
 import torch  # noqa: E402
 
 import invsim  # noqa: E402
@@ -40,16 +47,33 @@ def main():
     po, pr, pt, pu = obs.data_ptr(), rew.data_ptr(), te.data_ptr(), tr.data_ptr()
     hip = _capi.C.CDLL("libamdhip64.so")
 
+    C = _capi.C
+    raw0, raw1 = C.c_void_p(), C.c_void_p()
+    hip.hipEventCreate(C.byref(raw0))
+    hip.hipEventCreate(C.byref(raw1))
+    hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+    spv = C.c_void_p(sp)
+
     def region(K, wait):
         torch.cuda.synchronize(dev)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
+        if wait == "evpre":                  # the lazy event creation happens before the region
+            e0.record(stream)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        e0.record(stream)
+        if wait == "rawev":
+            hip.hipEventRecord(raw0, spv)
+        elif wait != "noev":
+            e0.record(stream)
         for i in range(K):
             lib.invsim_step(h, ptrs[i % 16], po, pr, pt, pu, None, sp)
-        e1.record(stream)
-        if wait == "sync":
+        if wait == "rawev":
+            hip.hipEventRecord(raw1, spv)
+        elif wait != "noev":
+            e1.record(stream)
+        if wait in ("sync", "noev", "evpre", "rawev"):
             torch.cuda.synchronize(dev)
         elif wait == "spin":
             while not e1.query():
@@ -59,12 +83,16 @@ def main():
             hip.hipStreamSynchronize(_capi.C.c_void_p(sp))
             torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
-        return el * 1e6, e0.elapsed_time(e1) * 1e3
+        if wait == "rawev":
+            ms = C.c_float()
+            hip.hipEventElapsedTime(C.byref(ms), raw0, raw1)
+            return el * 1e6, ms.value * 1e3
+        return el * 1e6, (e0.elapsed_time(e1) * 1e3 if wait != "noev" else 0.0)
 
     for _ in range(50):
         region(20, "sync")
-    for K in (0, 1, 20, 200, 2000):
-        for wait in ("sync", "spin", "stream"):
+    for K in (0, 1, 20, 200):
+        for wait in ("sync", "noev", "evpre", "rawev", "spin"):
             w, k = zip(*[region(K, wait) for _ in range(15)])
             w, k = sorted(w), sorted(k)
             print(f"K={K:5d} wait={wait:6s} wall_us med={w[7]:9.1f} min={w[0]:9.1f}  "
