@@ -71,10 +71,14 @@ __device__ __forceinline__ void spec_demand(Pcg &g, const PtrsConst (&pc)[G::RL]
 // One step (:436-635) at period t < T given the step's market demands Dd; obs
 // row into orow (LDS).  Returns the reward; Rn receives R[t] (the fulfilled
 // orders) per link.
-template <class G, bool WIN = true>
-__device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apow, NetSt<G> &s,
-                                           const float (&act)[G::E], const double (&Dd)[G::RL], float *orow,
-                                           double (&Rn)[G::E], double *met, double *irec) {
+//
+// spec_core: the step without the observation, given each link's age-L window
+// entry wa[k] = R[t - L_k] (the arrival; unused for L == 0).
+template <class G>
+__device__ __forceinline__ double spec_core(const NetParams &P, double apow, NetSt<G> &s,
+                                            const float (&act)[G::E], const double (&Dd)[G::RL],
+                                            const double (&wa)[G::E], double (&Rn)[G::E], double *met,
+                                            double *irec) {
     double cons[G::J];
 #pragma unroll
     for (int j = 0; j < G::J; j++) cons[j] = 0.0;
@@ -104,7 +108,7 @@ __device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apo
     double arrv[G::E];
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
-        arrv[k] = (G::L[k] == 0) ? Rn[k] : s.w[G::ring_off[k] + (G::L[k] > 0 ? G::L[k] : 1) - 1];
+        arrv[k] = (G::L[k] == 0) ? Rn[k] : wa[k];
         s.Y[k] = s.Y[k] - arrv[k] + Rn[k];
     }
     // arrivals in predecessor adjacency order (:516-523); X[t+1] (:528)
@@ -184,6 +188,17 @@ __device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apo
         if (irec) irec[2 * G::RL + G::J + 2 * G::E + j] = pj;   // P[t, node]
         total += pj;
     }
+    return apow * total;                                       // :619
+}
+
+template <class G, bool WIN = true>
+__device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apow, NetSt<G> &s,
+                                           const float (&act)[G::E], const double (&Dd)[G::RL], float *orow,
+                                           double (&Rn)[G::E], double *met, double *irec) {
+    double wa[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) wa[k] = (G::L[k] > 0) ? s.w[G::L[k] > 0 ? G::ring_off[k] + G::L[k] - 1 : 0] : 0.0;
+    const double rw = spec_core<G>(P, apow, s, act, Dd, wa, Rn, met, irec);
     // obs (:334-413): U[t+1], X[t+1], then per link with L > 0 the fulfilled
     // orders R[t+1-L .. t] oldest first (ages L-1 .. 1, then R[t])
 #pragma unroll
@@ -201,7 +216,7 @@ __device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apo
         orow[G::win_off[k] + G::L[k] - 1] = (float)Rn[k];
     }
     (void)t;
-    return apow * total;                                       // :619
+    return rw;
 }
 
 // One step (:436-635) at period t < T: the demand draws, then the dynamics
@@ -984,6 +999,357 @@ net_roll_kernel(NetParams P, int t_start, StepIO<float, float> io) {
     }
 }
 
+// net_roll_kernel with the observation work moved to a third wave (for small
+// batches, where the dynamics wave has a SIMD to itself and its instruction
+// chain is the step time).  One 192-thread workgroup per 64 envs, three roles
+// pipelined over chunks of CH launch steps:
+//   wave 0 (demand)   the market demands into a ring of RD chunks, chunk c
+//                     complete before barrier c; a flat loop of one PTRS
+//                     candidate per lane and iteration, so lanes run ahead of
+//                     each other's rejections (up to the ring's depth) instead
+//                     of every draw waiting for the wave's slowest lane
+//   wave 1 (dynamics) consumes chunk c between barriers c and c + 1: spec_core
+//                     with the fulfilled orders in an LDS ring per link and
+//                     lane, slot (t mod L) (the arrival R[t - L] is read from
+//                     the slot this step's R[t] then overwrites; ring rows
+//                     older than the episode are masked at use by t >= L, so a
+//                     reset zeroes nothing); hands U[t+1], X[t+1] and R[t] of
+//                     every step to wave 2 as f32 (the obs dtype) in rec[c & 1]
+//   wave 2 (obs)      builds the observations of chunk c between barriers c + 1
+//                     and c + 2: the order windows (ages 1 .. L-1, f32, in
+//                     registers aligned by age), the LDS tile and its store
+// The dynamics wave no longer shifts 61 f64 window registers, converts them
+// to f32 or stores the tile each step.  Same arithmetic, in the same order,
+// as net_spec_kernel.
+template <class G>
+struct NetLpos {
+    static constexpr int count() {
+        int n = 0;
+        for (int k = 0; k < G::E; k++) n += G::L[k] > 0 ? 1 : 0;
+        return n;
+    }
+    static constexpr int sumL1() {   // obs window entries older than R[t]
+        int n = 0;
+        for (int k = 0; k < G::E; k++) n += G::L[k] > 0 ? G::L[k] - 1 : 0;
+        return n;
+    }
+    // rank of link k among the links with L > 0 (its R[t] column in rec)
+    static constexpr int rank(int k) {
+        int n = 0;
+        for (int q = 0; q < k; q++) n += G::L[q] > 0 ? 1 : 0;
+        return n;
+    }
+    // first age-1 register of link k's f32 window (ages 1 .. L-1)
+    static constexpr int woff(int k) {
+        int n = 0;
+        for (int q = 0; q < k; q++) n += G::L[q] > 0 ? G::L[q] - 1 : 0;
+        return n;
+    }
+};
+
+#ifndef NET_ROLL3_CH
+#define NET_ROLL3_CH 2   // chunk of the 3-role rollout (LDS: two 192-thread workgroups per CU)
+#endif
+#ifndef NET_ROLL3_RD
+#define NET_ROLL3_RD 8   // demand ring depth in chunks (>= 2): how far the demand wave may run ahead
+#endif
+
+template <class G, int CH_>
+struct NetRoll3 {
+    static constexpr int CH = CH_;
+    static constexpr int NR = G::RL + G::J + NetLpos<G>::count();   // rec columns per step
+    static constexpr size_t tile_bytes() { return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float); }
+    static constexpr size_t rhs_bytes() { return (size_t)G::RL * RHS_LDS_MAX * sizeof(double); }
+    static constexpr int RD = NET_ROLL3_RD;
+    static constexpr size_t dbuf_bytes() { return (size_t)RD * CH * G::RL * WAVE * sizeof(double); }
+    static constexpr size_t ring_bytes() { return (size_t)(G::sumL > 0 ? G::sumL : 1) * WAVE * sizeof(double); }
+    static constexpr size_t rec_bytes() { return 2 * (size_t)CH * NR * WAVE * sizeof(float); }
+    static constexpr size_t lds() { return tile_bytes() + rhs_bytes() + dbuf_bytes() + ring_bytes() + rec_bytes(); }
+};
+
+template <class G, int CH_>
+__global__ void __launch_bounds__(3 * WAVE)
+net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
+    using R3 = NetRoll3<G, CH_>;
+    using LP = NetLpos<G>;
+    constexpr int O = G::O, CH = R3::CH, RD = R3::RD, RL = G::RL, NR = R3::NR;
+    constexpr int TILE_IT = (EPW * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
+    extern __shared__ __attribute__((aligned(16))) float n3_lds[];
+    char *lb = reinterpret_cast<char *>(n3_lds);
+    float *tile = n3_lds;
+    double *rhs_l = reinterpret_cast<double *>(lb + R3::tile_bytes());
+    double *dbuf = reinterpret_cast<double *>(lb + R3::tile_bytes() + R3::rhs_bytes());     // [RD * CH][RL][WAVE]
+    double *ring = reinterpret_cast<double *>(lb + R3::tile_bytes() + R3::rhs_bytes() + R3::dbuf_bytes());
+    float *rec = reinterpret_cast<float *>(lb + R3::tile_bytes() + R3::rhs_bytes() + R3::dbuf_bytes() +
+                                           R3::ring_bytes());                              // [2][CH][NR][WAVE]
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int role = threadIdx.x / WAVE;
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e = e0 + lane;
+    const bool valid = e < N;
+    const int64_t el = valid ? e : N - 1;       // padded lanes: the last env's data, never stored
+    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
+    const int K = io.K;
+    const int nch = (K + CH - 1) / CH;
+    if (role == 0) {   // ---- demand wave
+        PtrsConst pc[RL];
+#pragma unroll
+        for (int r = 0; r < RL; r++) pc[r] = P.rl_pc[r];
+        constexpr int NT = RHS_LDS_MAX / WAVE;
+        double tv[RL][NT];
+#pragma unroll
+        for (int r = 0; r < RL; r++) {
+            const int qm = pc[r].nk > 0 ? pc[r].nk - 1 : 0;
+            const double *src = pc[r].nk > 0 ? P.rhs + pc[r].toff : P.alpha_pow;   // any valid pointer
+#pragma unroll
+            for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
+        }
+        Pcg g = P.cm.rng.load(el);
+#pragma unroll
+        for (int r = 0; r < RL; r++)
+#pragma unroll
+            for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
+        wave_lds_sync();
+        // Flat draw loop: each lane works through its own draws (launch step j,
+        // retail link r), one PTRS candidate per iteration, so a rejection
+        // delays only its own lane; the wave passes barrier b as soon as every
+        // lane holds chunk b, and a lane runs ahead until the ring slot it
+        // needs is still being read (step j reuses step j - RD*CH's slot, which
+        // the dynamics wave is done with after barrier (j / CH - RD) + 1).
+        int j = 0, r = 0, t = t_start;
+        int b = 0;                                 // barriers passed
+        const int nb = nch + 1;                    // ... of nch + 1
+        for (;;) {
+            while (b < nb && __all(j >= min((b + 1) * CH, K))) {
+                net_wg_sync();                     // barrier b: demand chunk b ready
+                b++;
+            }
+            if (b == nb) break;
+            if (j < K && j / CH - RD + 2 <= b) {
+                if (t >= P.T) {                    // NEXT_STEP reset step: no draw
+                    t = 0;
+                    j++;
+                } else {
+                    PtrsConst c = pc[0];
+                    const double *rt = rhs_l;
+#pragma unroll
+                    for (int q = 1; q < RL; q++)
+                        if (r == q) {
+                            c = pc[q];
+                            rt = rhs_l + q * RHS_LDS_MAX;
+                        }
+                    int64_t kd = 0;
+                    bool acc = true;
+#ifdef INVSIM_ABL_ROLL_NO_DRAW
+                    kd = 20;
+#else
+                    if (c.lam >= 10)
+                        acc = ptrs_candidate(g, c, [&](int64_t kk, const PtrsConst &cc) { return ptrs_rhs(cc, rt, kk); },
+                                             kd);
+                    else if (c.lam == 0)
+                        kd = 0;
+                    else
+                        kd = np_poisson_mult(g, c.enlam);
+#endif
+                    if (acc) {                     // max(0, int(round(poisson(lam)))) (:536-541)
+                        dbuf[((j % (RD * CH)) * RL + r) * WAVE + lane] = (double)(kd > 0 ? kd : 0);
+                        if (++r == RL) {
+                            r = 0;
+                            j++;
+                            t++;
+                        }
+                    }
+                }
+            }
+        }
+        if (valid) P.cm.rng.store_state(e, g);
+        return;
+    }
+    if (role == 2) {   // ---- obs wave
+        float *trow = tile + lane * O;
+        int t = t_start;
+        // f32 order windows, ages 1 .. L-1: wf[woff(k) + a - 1] = R[t - a] (zeros before the episode)
+        float wf[LP::sumL1() > 0 ? LP::sumL1() : 1];
+#pragma unroll
+        for (int k = 0; k < G::E; k++) {
+            if (G::L[k] <= 1) continue;
+#pragma unroll
+            for (int a = 1; a < G::L[k]; a++) {
+                const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+                const double v = P.Rring[(int64_t)row * S + el];
+                wf[LP::woff(k) + a - 1] = (t - a >= 0) ? (float)v : 0.f;
+            }
+        }
+        net_wg_sync();   // barrier 0
+        for (int c = 0; c < nch; c++) {
+            net_wg_sync();   // barrier c + 1: record chunk c ready
+            const float *rb = rec + (c & 1) * CH * NR * WAVE;
+            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+                const int k = c * CH + kk;
+#ifdef INVSIM_ABL_R3_NO_OBS
+                continue;
+#endif
+                if (t >= P.T) {                    // NEXT_STEP autoreset: [0, I0, 0 ...] (:301-332)
+#pragma unroll
+                    for (int r = 0; r < RL; r++) trow[r] = 0.f;
+#pragma unroll
+                    for (int j = 0; j < G::J; j++) trow[RL + j] = (float)G::I0[j];
+#pragma unroll
+                    for (int q = 0; q < G::sumL; q++) trow[RL + G::J + q] = 0.f;
+#pragma unroll
+                    for (int q = 0; q < LP::sumL1(); q++) wf[q] = 0.f;
+                    t = 0;
+                } else {
+                    // obs (:334-413): U[t+1], X[t+1], then per link with L > 0
+                    // R[t+1-L .. t] oldest first (ages L-1 .. 1, then R[t])
+#pragma unroll
+                    for (int q = 0; q < RL + G::J; q++) trow[q] = rb[(kk * NR + q) * WAVE + lane];
+#pragma unroll
+                    for (int kl = 0; kl < G::E; kl++) {
+                        if (G::L[kl] == 0) continue;
+                        const float rn = rb[(kk * NR + RL + G::J + LP::rank(kl)) * WAVE + lane];
+#pragma unroll
+                        for (int p = 0; p + 1 < G::L[kl]; p++)
+                            trow[G::win_off[kl] + p] = wf[LP::woff(kl) + (G::L[kl] - 1 - p) - 1];
+                        trow[G::win_off[kl] + G::L[kl] - 1] = rn;
+                        // age the window: age a + 1 <- age a, age 1 <- R[t]
+#pragma unroll
+                        for (int a = G::L[kl] - 1; a >= 2; a--) wf[LP::woff(kl) + a - 1] = wf[LP::woff(kl) + a - 2];
+                        if (G::L[kl] > 1) wf[LP::woff(kl)] = rn;
+                    }
+                    t += 1;
+                }
+                wave_lds_sync();
+#ifndef INVSIM_ABL_ROLL_NO_STORE
+                store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+#endif
+                wave_lds_sync();
+            }
+        }
+        return;
+    }
+    // ---- dynamics wave
+    double *rg = ring + lane;                   // [sumL][WAVE]: R[t'] of link k at row ring_off[k] + t' mod L
+    int t = t_start;
+    NetSt<G> st;
+#pragma unroll
+    for (int j = 0; j < G::J; j++) st.X[j] = P.X[j * S + el];
+#pragma unroll
+    for (int r = 0; r < RL; r++) st.U[r] = P.U[r * S + el];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) st.Y[k] = P.Y[k * S + el];
+    {
+        double rv[G::sumL > 0 ? G::sumL : 1];
+#pragma unroll
+        for (int q = 0; q < G::sumL; q++) rv[q] = P.Rring[(int64_t)q * S + el];
+#pragma unroll
+        for (int q = 0; q < G::sumL; q++) rg[q * WAVE] = rv[q];
+    }
+    float nact[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) nact[k] = io.act[el * G::E + k];
+    double napow = P.alpha_pow[t < P.T ? t : 0];
+    double dlast[RL];
+#pragma unroll
+    for (int r = 0; r < RL; r++) dlast[r] = 0.0;
+    bool last_real = false;
+    double Rn[G::E];
+    net_wg_sync();   // barrier 0: demand chunk 0 ready
+    for (int c = 0; c < nch; c++) {
+        const double *db = dbuf + (c % RD) * CH * RL * WAVE;
+        float *rb = rec + (c & 1) * CH * NR * WAVE;
+        for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+            const int k = c * CH + kk;
+            const int64_t oi = (int64_t)k * N + e;
+            float act[G::E];
+#pragma unroll
+            for (int q = 0; q < G::E; q++) act[q] = nact[q];
+            const double apow = napow;
+            {
+                const int tn = (t >= P.T) ? 0 : t + 1;          // the next launch step's period
+                napow = P.alpha_pow[tn < P.T ? tn : 0];
+            }
+            if (k + 1 < K) {                                    // the next step's actions
+#pragma unroll
+                for (int q = 0; q < G::E; q++) nact[q] = io.act[((int64_t)(k + 1) * N + el) * G::E + q];
+            }
+            if (t >= P.T) {                                     // NEXT_STEP autoreset (:301-332)
+#pragma unroll
+                for (int j = 0; j < G::J; j++) st.X[j] = G::I0[j];
+#pragma unroll
+                for (int r = 0; r < RL; r++) st.U[r] = 0.0;
+#pragma unroll
+                for (int q = 0; q < G::E; q++) st.Y[q] = 0.0;
+                if (valid) {
+                    out_store(io.rew + oi, 0.0);
+                    out_store(io.term + oi, (uint8_t)0);
+                    out_store(io.trunc + oi, (uint8_t)0);
+                }
+                t = 0;
+            } else {
+                double Dd[RL], wa[G::E];
+#pragma unroll
+                for (int r = 0; r < RL; r++) Dd[r] = db[(kk * RL + r) * WAVE + lane];
+#pragma unroll
+                for (int q = 0; q < G::E; q++) {               // arrival R[t - L] (zero before the episode)
+                    if (G::L[q] == 0) {
+                        wa[q] = 0.0;
+                        continue;
+                    }
+                    const double v = rg[(G::ring_off[q] + (int)((uint32_t)t % (uint32_t)G::L[q])) * WAVE];
+                    wa[q] = (t >= G::L[q]) ? v : 0.0;
+                }
+                const double rw = spec_core<G>(P, apow, st, act, Dd, wa, Rn, nullptr, nullptr);
+#pragma unroll
+                for (int q = 0; q < G::E; q++)
+                    if (G::L[q] > 0) rg[(G::ring_off[q] + (int)((uint32_t)t % (uint32_t)G::L[q])) * WAVE] = Rn[q];
+#pragma unroll
+                for (int r = 0; r < RL; r++) rb[(kk * NR + r) * WAVE + lane] = (float)st.U[r];
+#pragma unroll
+                for (int j = 0; j < G::J; j++) rb[(kk * NR + RL + j) * WAVE + lane] = (float)st.X[j];
+#pragma unroll
+                for (int q = 0; q < G::E; q++)
+                    if (G::L[q] > 0) rb[(kk * NR + RL + G::J + LP::rank(q)) * WAVE + lane] = (float)Rn[q];
+                if (valid) {
+                    out_store(io.rew + oi, rw);
+                    out_store(io.term + oi, (uint8_t)0);
+                    out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.T ? 1 : 0));
+                }
+#pragma unroll
+                for (int r = 0; r < RL; r++) dlast[r] = Dd[r];
+                last_real = k == K - 1;
+                t += 1;
+            }
+        }
+        net_wg_sync();   // barrier c + 1: demand chunk c + 1 and record chunk c ready
+    }
+    if (valid) {
+#pragma unroll
+        for (int j = 0; j < G::J; j++) st_store(P.X + j * S + e, st.X[j]);
+#pragma unroll
+        for (int r = 0; r < RL; r++) st_store(P.U + r * S + e, st.U[r]);
+#pragma unroll
+        for (int k = 0; k < G::E; k++) st_store(P.Y + k * S + e, st.Y[k]);
+        // ring rows older than the episode are stored as zeros (the reference's zeroed history)
+#pragma unroll
+        for (int k = 0; k < G::E; k++) {
+            if (G::L[k] == 0) continue;
+#pragma unroll
+            for (int a = 1; a <= G::L[k]; a++) {
+                const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+                const double v = rg[row * WAVE];
+                st_store(P.Rring + (int64_t)row * S + e, (t - a >= 0) ? v : 0.0);
+            }
+        }
+        if (P.cm.info_demand && last_real) {
+#pragma unroll
+            for (int r = 0; r < RL; r++) P.cm.info_demand[e * RL + r] = (int64_t)dlast[r];
+        }
+    }
+}
+
 }  // namespace
 
 template <class G>
@@ -1020,6 +1386,17 @@ int net_spec_match(const invsim_netinvmgmt_spec &h) {
 static bool net_roll_enabled() {
     const char *v = getenv("INVSIM_NET_ROLL");
     return !(v && v[0] == '0');
+}
+
+// Rollout kernel choice: the 3-role net_roll3o_kernel for batches of at most
+// NET_ROLL3_MAX envs (a dynamics wave per SIMD or fewer), net_roll_kernel above.
+// INVSIM_NET_ROLL3=0 / 1 forces either (A/B measurements, tests).
+constexpr int64_t NET_ROLL3_MAX = 32768;
+static bool net_roll3_use(int64_t N) {
+    const char *v = getenv("INVSIM_NET_ROLL3");
+    if (v && v[0] == '0') return false;
+    if (v && v[0] == '1') return true;
+    return N <= NET_ROLL3_MAX;
 }
 
 template <class G>
@@ -1074,8 +1451,13 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
 #define K_(TU, ONE, POL) hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
     if (!pol && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
         (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
-        const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE)), br(2 * WAVE);
-        hipLaunchKernelGGL((net_roll_kernel<G>), gr, br, NetRoll<G>::lds(), s, p, t_u, io);
+        const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE));
+        if (net_roll3_use(p.cm.N)) {
+            using R3 = NetRoll3<G, NET_ROLL3_CH>;
+            hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io);
+        } else {
+            hipLaunchKernelGGL((net_roll_kernel<G>), gr, dim3(2 * WAVE), NetRoll<G>::lds(), s, p, t_u, io);
+        }
         return hipGetLastError();
     }
     if (pol) {

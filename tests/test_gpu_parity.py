@@ -958,10 +958,53 @@ def test_invmgmt_three_role_rollout_equals_two_role(gpu, monkeypatch, cls, n):
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
 
 
+@pytest.mark.parametrize("graph,backlog,n,periods,mode", [
+    ("default", True, 3000, 30, "next_step"),
+    ("default", False, 32768, 30, "next_step"),      # the BASELINE Net configuration
+    ("default", True, 1000, 4, "next_step"),         # several resets per chunk, t < L at every step
+    ("custom", True, 2000, 30, "next_step"),
+    ("custom", False, 777, 3, "next_step"),
+    ("default", True, 1000, 30, "disabled"),
+])
+def test_net_three_role_rollout_equals_two_role(gpu, monkeypatch, graph, backlog, n, periods, mode):
+    """Batches of at most 32 768 envs run net_roll3o_kernel (order rings in
+    LDS, obs work on a third wave); INVSIM_NET_ROLL3=0 keeps them on
+    net_roll_kernel.  Same state in: identical outputs, demand record and
+    state out, across rollouts that start mid-episode and cross resets."""
+    import invsim
+    from invsim.topology import custom_graph, default_graph
+    mk_g = default_graph if graph == "default" else custom_graph
+    envs = []
+    for i in range(2):
+        env = invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), backlog=backlog, num_periods=periods,
+                                         autoreset_mode=mode, record_demand=True)
+        env.reset(seed=23)
+        envs.append(env)
+    A = envs[0].action_dim
+    g = torch.Generator(device=gpu).manual_seed(4)
+    a = torch.rand((n, A), device=gpu, generator=g) * 250
+    for env in envs:
+        env.step(a)
+    Ks = (75, 9, 2) if mode == "next_step" else (8, 17)
+    for K in Ks:
+        a = torch.rand((K, n, A), device=gpu, generator=g) * 300 - 5
+        a[:, ::53, 0] = 2.5                    # half-to-even ties
+        outs, dems = [], []
+        for i, env in enumerate(envs):
+            monkeypatch.setenv("INVSIM_NET_ROLL3", "1" if i == 0 else "0")
+            outs.append(env.rollout(a))
+            dems.append(env._demand.clone())
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y), K
+        assert torch.equal(dems[0], dems[1])
+        assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
+    monkeypatch.delenv("INVSIM_NET_ROLL3")
+
+
 @pytest.mark.parametrize("family,cls_name,n", [
     ("im", "InvManagementBacklogEnv", 65536),       # im_roll3_kernel
     ("im", "InvManagementLostSalesEnv", 32768),     # im_roll3o_kernel (per-GPU shard of 262 144)
-    ("net", "NetInvMgmtBacklogEnv", 32768),         # net_roll_kernel, then net_step1_kernel
+    ("net", "NetInvMgmtBacklogEnv", 32768),         # net_roll3o_kernel, then net_step2_kernel
     ("nv", "NewsvendorEnv", 65536),                 # nv_roll_kernel
 ])
 def test_full_size_rollout_vs_oracle(gpu, oracle, family, cls_name, n):
