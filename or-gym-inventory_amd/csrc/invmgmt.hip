@@ -885,10 +885,11 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
 // K-step lock-step rollout (invsim_rollout, NEXT_STEP or DISABLED autoreset,
 // Poisson demand) for 3 stages with compile-time lead times L0..L2 (the
 // reference default [1, 5, 10]), one 128-thread workgroup per 64 envs:
-//   wave 0 (demand)   draws the demands of CH launch steps at a time into a
-//                     double-buffered LDS ring, ahead of the dynamics wave;
-//                     a demand is a function of the env's stream only, and a
-//                     NEXT_STEP reset step draws nothing (reset(), :186-222)
+//   wave 0 (demand)   draws the demands into an LDS ring of RD chunks of CH
+//                     launch steps, ahead of the dynamics wave, as a flat
+//                     per-lane loop (stream_flat_loop); a demand is a function
+//                     of the env's stream only, and a NEXT_STEP reset step
+//                     draws nothing (reset(), :186-222)
 //   wave 1 (dynamics) the step (:224-352) with every window in registers,
 //                     aligned by age: the fulfilled-order history of stage i
 //                     (rw_i[a] = R[t - L_i + a], so the arrival is rw_i[0]) and
@@ -901,16 +902,35 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
 // barrier c; the dynamics wave consumes chunk c after barrier c, so the
 // demand wave's refill of a buffer follows the dynamics wave's use of it.
 // Same arithmetic, in the same order, as im_step_regs.
+// The demand wave of the rollout kernels (stream_flat_loop): Poisson demand
+// (:280) of each launch step into the ring dbuf [RD * CH][WAVE], nb barriers
+template <int CH, int RD>
+__device__ __forceinline__ void im_stream_loop(const ImParams &P, Pcg &g, const double *rhs_l, int64_t *dbuf,
+                                               int lane, int K, int nb, int t_start) {
+    stream_flat_loop<CH, RD, 1>(
+        K, nb, t_start, P.periods,
+        [&](int, int64_t &d) {
+#ifdef INVSIM_ABL_ROLL_NO_DRAW
+            d = 20;
+            return true;
+#else
+            return np_poisson_try(g, P.pc, rhs_l, d);
+#endif
+        },
+        [&](int slot, int, int64_t d) { dbuf[slot * WAVE + lane] = d < 0 ? 0 : d; });
+}
+
 template <int L0, int L1, int L2>
 struct ImLt3 {
     static constexpr int M1 = 3;
     static constexpr int D = (L0 > L1 ? (L0 > L2 ? L0 : L2) : (L1 > L2 ? L1 : L2));
     static constexpr int O = M1 * (D + 1);
     static constexpr int CH = 8;                                         // demand chunk (launch steps)
+    static constexpr int RD = 4;                                         // demand ring depth (chunks)
     static constexpr int lt(int i) { return i == 0 ? L0 : i == 1 ? L1 : L2; }
     static constexpr int W(int i) { return lt(i) > 0 ? lt(i) : 1; }      // register window length
     static constexpr size_t lds() {
-        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + 2 * CH * WAVE * 8;
+        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8;
     }
 };
 
@@ -921,7 +941,7 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
     constexpr int M1 = G::M1, D = G::D, O = G::O, CH = G::CH;
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
     double *rhs_l = reinterpret_cast<double *>(im_tile + WAVE * O);
-    int64_t *dbuf = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);   // [2][CH][WAVE]
+    int64_t *dbuf = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);   // [RD * CH][WAVE]
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t N = P.cm.N;
     const int64_t S = P.cm.Npad;
@@ -944,24 +964,7 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
         }
         Pcg g = P.cm.rng.load(el);
         ts.flush(lane);
-        int t = t_start;
-        for (int c = 0; c < nch; c++) {
-            int64_t *db = dbuf + (c & 1) * CH * WAVE;
-            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
-                if (t >= P.periods) {              // NEXT_STEP reset step: no draw
-                    t = 0;
-                    continue;
-                }
-#ifdef INVSIM_ABL_ROLL_NO_DRAW
-                int64_t d = 20;
-#else
-                int64_t d = env_poisson(g, P.pc, rhs_l);                // :280
-#endif
-                db[kk * WAVE + lane] = d < 0 ? 0 : d;
-                t++;
-            }
-            wg_lds_sync();   // barrier c: chunk c ready
-        }
+        im_stream_loop<CH, G::RD>(P, g, rhs_l, dbuf, lane, K, nch, t_start);   // barriers 0 .. nch - 1
         if (valid) P.cm.rng.store_state(e, g);
         return;
     }
@@ -1004,7 +1007,7 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
     bool last_real = false;
     wg_lds_sync();   // barrier 0: chunk 0 ready
     for (int c = 0; c < nch; c++) {
-        const int64_t *db = dbuf + (c & 1) * CH * WAVE;
+        const int64_t *db = dbuf + (c % G::RD) * CH * WAVE;
         for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
             const int k = c * CH + kk;
             const int64_t oi = (int64_t)k * N + e;
@@ -1157,9 +1160,10 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
 // batches, where a dynamics wave has a SIMD to itself and its instruction
 // chain is the step time): one 192-thread workgroup per 64 envs, three roles
 // pipelined over chunks of CH launch steps:
-//   wave 0 (demand)   draws the demands of chunk c + 1 into a double-buffered
-//                     LDS ring; a demand is a function of the env's stream only,
-//                     and a NEXT_STEP reset step draws nothing (:186-222)
+//   wave 0 (demand)   draws the demands up to RD chunks ahead into an LDS
+//                     ring (stream_flat_loop); a demand is a function of the
+//                     env's stream only, and a NEXT_STEP reset step draws
+//                     nothing (:186-222)
 //   wave 1 (dynamics) consumes chunk c: the step (:224-352) with the
 //                     fulfilled-order history in registers aligned by age
 //                     (rw_i[a] = R[t - L_i + a], so the arrival is rw_i[0]);
@@ -1178,9 +1182,10 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
 template <int L0, int L1, int L2>
 struct ImLt3o : ImLt3<L0, L1, L2> {
     static constexpr int CH = 4;                                         // chunk (launch steps)
+    static constexpr int RD = 4;                                         // demand ring depth (chunks)
     static constexpr int M1 = 3, O = ImLt3<L0, L1, L2>::O;
     static constexpr size_t lds() {
-        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + 2 * CH * WAVE * 8 + 2 * CH * M1 * WAVE * 8;
+        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + 2 * CH * M1 * WAVE * 8;
     }
 };
 
@@ -1191,8 +1196,8 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
     constexpr int M1 = G::M1, D = G::D, O = G::O, CH = G::CH;
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
     double *rhs_l = reinterpret_cast<double *>(im_tile + WAVE * O);
-    int64_t *dbuf = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);   // [2][CH][WAVE]
-    int64_t *ibuf = dbuf + 2 * CH * WAVE;                                 // [2][CH][M1][WAVE]
+    int64_t *dbuf = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);   // [RD * CH][WAVE]
+    int64_t *ibuf = dbuf + G::RD * CH * WAVE;                             // [2][CH][M1][WAVE]
     const int lane = threadIdx.x & (WAVE - 1);
     const int role = threadIdx.x / WAVE;
     const int64_t N = P.cm.N;
@@ -1216,25 +1221,8 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
         }
         Pcg g = P.cm.rng.load(el);
         ts.flush(lane);
-        int t = t_start;
-        for (int c = 0; c < nch; c++) {
-            int64_t *db = dbuf + (c & 1) * CH * WAVE;
-            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
-                if (t >= P.periods) {              // NEXT_STEP reset step: no draw
-                    t = 0;
-                    continue;
-                }
-#ifdef INVSIM_ABL_ROLL_NO_DRAW
-                int64_t d = 20;
-#else
-                int64_t d = env_poisson(g, P.pc, rhs_l);                // :280
-#endif
-                db[kk * WAVE + lane] = d < 0 ? 0 : d;
-                t++;
-            }
-            wg_lds_sync();   // barrier c: demand chunk c ready
-        }
-        wg_lds_sync();       // barrier nch: the obs wave's last chunk
+        // barriers 0 .. nch - 1 (demand chunk c ready), nch (the obs wave's last chunk)
+        im_stream_loop<CH, G::RD>(P, g, rhs_l, dbuf, lane, K, nch + 1, t_start);
         if (valid) P.cm.rng.store_state(e, g);
         return;
     }
@@ -1347,7 +1335,7 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
     bool last_real = false;
     wg_lds_sync();   // barrier 0: demand chunk 0 ready
     for (int c = 0; c < nch; c++) {
-        const int64_t *db = dbuf + (c & 1) * CH * WAVE;
+        const int64_t *db = dbuf + (c % G::RD) * CH * WAVE;
         int64_t *ib = ibuf + (c & 1) * CH * M1 * WAVE;
         for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
             const int k = c * CH + kk;

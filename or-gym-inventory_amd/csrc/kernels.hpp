@@ -287,6 +287,65 @@ __device__ __forceinline__ void store_tile(const T *__restrict__ tile, T *__rest
     for (int64_t i = lane; i < count; i += WAVE) out_store(dst + i, tile[i]);
 }
 
+// Cross-wave LDS handoff inside a workgroup: orders LDS traffic only (an
+// __syncthreads() would also drain each wave's outstanding global loads and
+// stores, s_waitcnt vmcnt(0), before the s_barrier)
+__device__ __forceinline__ void roll_wg_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// One numpy random_poisson attempt for a fixed-rate stream: a PTRS candidate
+// (lam >= 10; false = rejected, the next attempt continues the stream), or the
+// whole multiplication-method draw (0 < lam < 10), or 0 (lam == 0) -- the
+// branches of np_poisson, so the attempts up to the first `true` consume the
+// stream exactly as one np_poisson call.
+__device__ __forceinline__ bool np_poisson_try(Pcg &g, const PtrsConst &c, const double *rhs, int64_t &k) {
+    if (c.lam >= 10) return ptrs_candidate(g, c, [&](int64_t kk, const PtrsConst &cc) { return ptrs_rhs(cc, rhs, kk); }, k);
+    k = (c.lam == 0) ? 0 : np_poisson_mult(g, c.enlam);
+    return true;
+}
+
+// The stream wave of a lock-step rollout kernel as a flat loop: each lane
+// works through its own demand draws (launch step j, draw r of the step's RL),
+// one attempt per iteration, so a PTRS rejection delays only its own lane
+// instead of every draw waiting for the wave's slowest lane.  Draws go to a
+// ring of RD chunks of CH launch steps (slot j mod RD*CH).  The consumer reads
+// chunk c between barriers c and c + 1; the wave passes barrier b (of nb) as
+// soon as every lane has drawn chunk b, and a lane may draw step j only once
+// the consumer is done with the slot's previous step j - RD*CH (barrier
+// (j / CH - RD) + 1 passed).  A NEXT_STEP reset step (t >= T) draws nothing.
+//   draw(r, k) -> bool: one attempt for draw r; put(slot, r, k): store it
+template <int CH, int RD, int RL, class Draw, class Put>
+__device__ __forceinline__ void stream_flat_loop(int K, int nb, int t, int T, Draw draw, Put put) {
+    static_assert(RD >= 2, "the ring needs two chunks");
+    int j = 0, r = 0, b = 0;
+    for (;;) {
+        while (b < nb && __all(j >= min((b + 1) * CH, K))) {
+            roll_wg_sync();                        // barrier b: chunk b drawn
+            b++;
+        }
+        if (b == nb) break;
+        if (j < K && j / CH - RD + 2 <= b) {
+            if (t >= T) {
+                t = 0;
+                j++;
+            } else {
+                int64_t kd = 0;
+                if (draw(r, kd)) {
+                    put((j % (RD * CH)), r, kd);
+                    if (++r == RL) {
+                        r = 0;
+                        j++;
+                        t++;
+                    }
+                }
+            }
+        }
+    }
+}
+
 // launchers (return hipGetLastError() of the launch)
 hipError_t seed_range_launch(const Common &cm, uint64_t base_lo, uint64_t base_hi, int64_t first,
                              const uint8_t *mask, hipStream_t s);

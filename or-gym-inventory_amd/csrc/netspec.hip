@@ -1112,58 +1112,28 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
 #pragma unroll
             for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
         wave_lds_sync();
-        // Flat draw loop: each lane works through its own draws (launch step j,
-        // retail link r), one PTRS candidate per iteration, so a rejection
-        // delays only its own lane; the wave passes barrier b as soon as every
-        // lane holds chunk b, and a lane runs ahead until the ring slot it
-        // needs is still being read (step j reuses step j - RD*CH's slot, which
-        // the dynamics wave is done with after barrier (j / CH - RD) + 1).
-        int j = 0, r = 0, t = t_start;
-        int b = 0;                                 // barriers passed
-        const int nb = nch + 1;                    // ... of nch + 1
-        for (;;) {
-            while (b < nb && __all(j >= min((b + 1) * CH, K))) {
-                net_wg_sync();                     // barrier b: demand chunk b ready
-                b++;
-            }
-            if (b == nb) break;
-            if (j < K && j / CH - RD + 2 <= b) {
-                if (t >= P.T) {                    // NEXT_STEP reset step: no draw
-                    t = 0;
-                    j++;
-                } else {
-                    PtrsConst c = pc[0];
-                    const double *rt = rhs_l;
+        // flat draw loop (stream_flat_loop): up to RD chunks ahead of the dynamics
+        stream_flat_loop<CH, RD, RL>(
+            K, nch + 1, t_start, P.T,
+            [&](int r, int64_t &kd) {
+                PtrsConst c = pc[0];
+                const double *rt = rhs_l;
 #pragma unroll
-                    for (int q = 1; q < RL; q++)
-                        if (r == q) {
-                            c = pc[q];
-                            rt = rhs_l + q * RHS_LDS_MAX;
-                        }
-                    int64_t kd = 0;
-                    bool acc = true;
-#ifdef INVSIM_ABL_ROLL_NO_DRAW
-                    kd = 20;
-#else
-                    if (c.lam >= 10)
-                        acc = ptrs_candidate(g, c, [&](int64_t kk, const PtrsConst &cc) { return ptrs_rhs(cc, rt, kk); },
-                                             kd);
-                    else if (c.lam == 0)
-                        kd = 0;
-                    else
-                        kd = np_poisson_mult(g, c.enlam);
-#endif
-                    if (acc) {                     // max(0, int(round(poisson(lam)))) (:536-541)
-                        dbuf[((j % (RD * CH)) * RL + r) * WAVE + lane] = (double)(kd > 0 ? kd : 0);
-                        if (++r == RL) {
-                            r = 0;
-                            j++;
-                            t++;
-                        }
+                for (int q = 1; q < RL; q++)
+                    if (r == q) {
+                        c = pc[q];
+                        rt = rhs_l + q * RHS_LDS_MAX;
                     }
-                }
-            }
-        }
+#ifdef INVSIM_ABL_ROLL_NO_DRAW
+                kd = 20;
+                return true;
+#else
+                return np_poisson_try(g, c, rt, kd);
+#endif
+            },
+            [&](int slot, int r, int64_t kd) {   // max(0, int(round(poisson(lam)))) (:536-541)
+                dbuf[(slot * RL + r) * WAVE + lane] = (double)(kd > 0 ? kd : 0);
+            });
         if (valid) P.cm.rng.store_state(e, g);
         return;
     }
