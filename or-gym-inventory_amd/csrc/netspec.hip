@@ -68,6 +68,35 @@ __device__ __forceinline__ void spec_demand(Pcg &g, const PtrsConst (&pc)[G::RL]
     }
 }
 
+// The demand wave of the rollout kernels (stream_flat_loop): the market demands
+// of each launch step, retail-link order, into the ring dbuf [RD * CH][RL][WAVE]
+template <class G, int CH, int RD>
+__device__ __forceinline__ void net_demand_loop(Pcg &g, const PtrsConst (&pc)[G::RL], const double *rhs_l,
+                                                double *dbuf, int lane, int K, int nb, int t_start, int T) {
+    constexpr int RL = G::RL;
+    stream_flat_loop<CH, RD, RL>(
+        K, nb, t_start, T,
+        [&](int r, int64_t &kd) {
+            PtrsConst c = pc[0];
+            const double *rt = rhs_l;
+#pragma unroll
+            for (int q = 1; q < RL; q++)
+                if (r == q) {
+                    c = pc[q];
+                    rt = rhs_l + q * RHS_LDS_MAX;
+                }
+#ifdef INVSIM_ABL_ROLL_NO_DRAW
+            kd = 20;
+            return true;
+#else
+            return np_poisson_try(g, c, rt, kd);
+#endif
+        },
+        [&](int slot, int r, int64_t kd) {   // max(0, int(round(poisson(lam)))) (:536-541)
+            dbuf[(slot * RL + r) * WAVE + lane] = (double)(kd > 0 ? kd : 0);
+        });
+}
+
 // One step (:436-635) at period t < T given the step's market demands Dd; obs
 // row into orow (LDS).  Returns the reward; Rn receives R[t] (the fulfilled
 // orders) per link.
@@ -815,23 +844,25 @@ __global__ void __launch_bounds__(256) net_commit_kernel(NetParams P, int slot, 
 // autoreset or no overrun, Poisson market demand) of a compiled network, one
 // 128-thread workgroup per 64 envs:
 //   wave 0 (demand)   draws the market demands (RL per step, retail-link order)
-//                     of CH launch steps at a time into a double-buffered LDS
-//                     ring, ahead of the dynamics wave.  A demand is a function
+//                     into an LDS ring of RD chunks of CH launch steps, ahead
+//                     of the dynamics wave (net_demand_loop).  A demand is a function
 //                     of the env's stream only (the orders never touch it), and
 //                     a NEXT_STEP reset step draws nothing (reset(), :301-332).
 //   wave 1 (dynamics) spec_dyn with the windows in registers; a step's actions
 //                     and alpha**t are loaded one step ahead, before the
 //                     previous step's stores (vmcnt is in order: a load issued
 //                     behind stores waits for them).
-// Chunk handoff: the demand wave fills buffer c & 1, then barrier c; the
-// dynamics wave consumes chunk c after barrier c, so a buffer's refill follows
-// its use.  Same arithmetic, in the same order, as net_spec_kernel.
+// Chunk handoff: chunk c is in the ring before barrier c; the dynamics wave
+// consumes it between barriers c and c + 1, and the demand wave refills its
+// slots only after barrier c + 1.  Same arithmetic, in the same order, as
+// net_spec_kernel.
 template <class G>
 struct NetRoll {
     static constexpr int CH = 8;                                          // demand chunk (launch steps)
+    static constexpr int RD = 4;                                          // demand ring depth (chunks)
     static constexpr size_t tile_bytes() { return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float); }
     static constexpr size_t lds() {
-        return tile_bytes() + (size_t)G::RL * RHS_LDS_MAX * sizeof(double) + 2 * (size_t)CH * G::RL * WAVE * sizeof(double);
+        return tile_bytes() + (size_t)G::RL * RHS_LDS_MAX * sizeof(double) + (size_t)RD * CH * G::RL * WAVE * sizeof(double);
     }
 };
 
@@ -844,7 +875,7 @@ net_roll_kernel(NetParams P, int t_start, StepIO<float, float> io) {
     extern __shared__ __attribute__((aligned(16))) float nr_lds[];
     float *tile = nr_lds;
     double *rhs_l = reinterpret_cast<double *>(nr_lds + R::tile_bytes() / sizeof(float));
-    double *dbuf = rhs_l + RL * RHS_LDS_MAX;                          // [2][CH][RL][WAVE]
+    double *dbuf = rhs_l + RL * RHS_LDS_MAX;                          // [RD * CH][RL][WAVE]
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t N = P.cm.N;
     const int64_t S = P.cm.Npad;
@@ -874,26 +905,7 @@ net_roll_kernel(NetParams P, int t_start, StepIO<float, float> io) {
 #pragma unroll
             for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
         wave_lds_sync();
-        int t = t_start;
-        for (int c = 0; c < nch; c++) {
-            double *db = dbuf + (c & 1) * CH * RL * WAVE;
-            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
-                if (t >= P.T) {                    // NEXT_STEP reset step: no draw
-                    t = 0;
-                    continue;
-                }
-                double Dd[RL];
-#ifdef INVSIM_ABL_ROLL_NO_DRAW
-                for (int r = 0; r < RL; r++) Dd[r] = 20.0;
-#else
-                spec_demand<G>(g, pc, rhs_l, Dd);
-#endif
-#pragma unroll
-                for (int r = 0; r < RL; r++) db[(kk * RL + r) * WAVE + lane] = Dd[r];
-                t++;
-            }
-            net_wg_sync();   // barrier c: chunk c ready
-        }
+        net_demand_loop<G, CH, R::RD>(g, pc, rhs_l, dbuf, lane, K, nch, t_start, P.T);   // barriers 0 .. nch - 1
         if (valid) P.cm.rng.store_state(e, g);
         return;
     }
@@ -928,7 +940,7 @@ net_roll_kernel(NetParams P, int t_start, StepIO<float, float> io) {
     double Rn[G::E];
     net_wg_sync();   // barrier 0: chunk 0 ready
     for (int c = 0; c < nch; c++) {
-        const double *db = dbuf + (c & 1) * CH * RL * WAVE;
+        const double *db = dbuf + (c % R::RD) * CH * RL * WAVE;
         for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
             const int k = c * CH + kk;
             const int64_t oi = (int64_t)k * N + e;
@@ -1112,28 +1124,9 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
 #pragma unroll
             for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
         wave_lds_sync();
-        // flat draw loop (stream_flat_loop): up to RD chunks ahead of the dynamics
-        stream_flat_loop<CH, RD, RL>(
-            K, nch + 1, t_start, P.T,
-            [&](int r, int64_t &kd) {
-                PtrsConst c = pc[0];
-                const double *rt = rhs_l;
-#pragma unroll
-                for (int q = 1; q < RL; q++)
-                    if (r == q) {
-                        c = pc[q];
-                        rt = rhs_l + q * RHS_LDS_MAX;
-                    }
-#ifdef INVSIM_ABL_ROLL_NO_DRAW
-                kd = 20;
-                return true;
-#else
-                return np_poisson_try(g, c, rt, kd);
-#endif
-            },
-            [&](int slot, int r, int64_t kd) {   // max(0, int(round(poisson(lam)))) (:536-541)
-                dbuf[(slot * RL + r) * WAVE + lane] = (double)(kd > 0 ? kd : 0);
-            });
+        // flat draw loop (stream_flat_loop): up to RD chunks ahead of the dynamics;
+        // barriers 0 .. nch - 1 (demand chunk c ready), nch (the obs wave's last chunk)
+        net_demand_loop<G, CH, RD>(g, pc, rhs_l, dbuf, lane, K, nch + 1, t_start, P.T);
         if (valid) P.cm.rng.store_state(e, g);
         return;
     }
