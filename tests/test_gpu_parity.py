@@ -961,15 +961,15 @@ def test_invmgmt_three_role_rollout_equals_two_role(gpu, monkeypatch, cls, n):
 @pytest.mark.parametrize("graph,backlog,n,periods,mode", [
     ("default", True, 3000, 30, "next_step"),
     ("default", False, 32768, 30, "next_step"),      # the BASELINE Net configuration
+    ("default", True, 65536, 30, "next_step"),       # two workgroup rounds (LDS: two per CU)
     ("default", True, 1000, 4, "next_step"),         # several resets per chunk, t < L at every step
     ("custom", True, 2000, 30, "next_step"),
     ("custom", False, 777, 3, "next_step"),
     ("default", True, 1000, 30, "disabled"),
 ])
 def test_net_three_role_rollout_equals_two_role(gpu, monkeypatch, graph, backlog, n, periods, mode):
-    """Batches of at most 32 768 envs run net_roll3o_kernel (order rings in
-    LDS, obs work on a third wave); INVSIM_NET_ROLL3=0 keeps them on
-    net_roll_kernel.  Same state in: identical outputs, demand record and
+    """Compiled-network rollouts run net_roll3o_kernel (order rings in LDS, obs
+    work on a third wave); INVSIM_NET_ROLL3=0 keeps them on net_roll_kernel.  Same state in: identical outputs, demand record and
     state out, across rollouts that start mid-episode and cross resets."""
     import invsim
     from invsim.topology import custom_graph, default_graph
