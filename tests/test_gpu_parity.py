@@ -1057,6 +1057,56 @@ def test_full_size_rollout_vs_oracle(gpu, oracle, family, cls_name, n):
         oracle.set_threads(1)
 
 
+@pytest.mark.parametrize("family,lam", [(f, lam) for f in ("im3o", "im3", "net3o", "net3o_custom")
+                                         for lam in (0.0, 4.0, 9.99, 10.0, 162.6540478400545)])
+def test_flat_stream_rollout_rates_vs_oracle(gpu, oracle, monkeypatch, family, lam):
+    """The rollout kernels' flat demand loops (stream_flat_loop) under every
+    branch of numpy's Poisson sampler: lam = 0 (no draw), 0 < lam < 10 (the
+    multiplication method as one attempt), lam >= 10 (PTRS, one candidate per
+    attempt), across NEXT_STEP resets inside the launch: bit-exact obs,
+    rewards and flags against the C oracle stepping the same seeds."""
+    import invsim
+    from invsim.topology import custom_graph, default_graph
+    n, T = 1000, 7
+    rng = np.random.default_rng(13)
+    if family.startswith("im"):
+        if family == "im3":
+            monkeypatch.setenv("INVSIM_IM_ROLL3O_MAX_N", "0")      # the 2-role im_roll3_kernel
+        env = invsim.InvManagementBacklogEnv(n, device=gpu, periods=T, dist_param={"mu": lam})
+        orc = oracle.OracleInvMgmt(n, periods=T, dist_param={"mu": lam})
+        K = 40
+        acts = np.stack([_im_random_actions(rng, n, 3, [100, 200, 230]) for _ in range(K)])
+    else:
+        custom = family.endswith("custom")
+        g = (custom_graph if custom else default_graph)(demand_lam=lam)
+        og = (oracle.custom_graph if custom else oracle.default_graph)()
+        for u, v, a in og.edges(data=True):
+            if "dist_param" in a:
+                a["dist_param"] = {"lam": lam}
+        env = invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=g, num_periods=T)
+        orc = oracle.OracleNet(n, graph=og, num_periods=T)
+        K = 40
+        acts = rng.uniform(-5, 300, size=(K, n, env.action_dim)).astype(np.float32)
+    orc.seed(range(500, 500 + n))
+    e_obs = orc.reset()
+    obs, _ = env.reset(seed=500)
+    assert _eq_bits(obs.cpu().numpy(), e_obs)
+    o, r, te, tr = env.rollout(torch.from_numpy(acts).to(gpu))
+    o, r, tr = o.cpu().numpy(), r.cpu().numpy(), tr.cpu().numpy()
+    t = 0
+    for k in range(K):
+        if t >= T:                                  # NEXT_STEP autoreset step
+            assert _eq_bits(o[k], orc.reset()), k
+            assert (r[k] == 0).all() and not tr[k].any(), k
+            t = 0
+            continue
+        res = orc.step(acts[k])
+        assert _eq_bits(o[k], res[0]), f"obs step {k}"
+        _assert_reward(r[k], res[1], f"step {k}")
+        assert np.array_equal(tr[k], res[2]), k
+        t += 1
+
+
 @pytest.mark.parametrize("mu_max,step_limit", [(9.0, 40), (14.0, 6), (40.0, 13), (60.0, 40), (100.0, 40),
                                              (200.0, 5), (400.0, 40)])
 def test_newsvendor_rollout_sampler_mixes(gpu, monkeypatch, mu_max, step_limit):
