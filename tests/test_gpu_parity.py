@@ -729,21 +729,25 @@ def test_newsvendor_demand_lookahead_mixed_calls(gpu, kw, monkeypatch):
     same_state()
 
 
-@pytest.mark.parametrize("cls,n,pre,Ks,mode", [
-    ("InvManagementBacklogEnv", 4000, 0, (75, 2, 9), "next_step"),
-    ("InvManagementLostSalesEnv", 4000, 7, (40, 16, 3), "next_step"),
-    ("InvManagementBacklogEnv", 65536, 3, (61,), "next_step"),
-    ("InvManagementBacklogEnv", 1000, 5, (8, 17), "disabled"),
+@pytest.mark.parametrize("cls,n,pre,Ks,mode,periods", [
+    ("InvManagementBacklogEnv", 4000, 0, (75, 2, 9), "next_step", 30),
+    ("InvManagementLostSalesEnv", 4000, 7, (40, 16, 3), "next_step", 30),
+    ("InvManagementBacklogEnv", 65536, 3, (61,), "next_step", 30),
+    ("InvManagementBacklogEnv", 1000, 5, (8, 17), "disabled", 30),
+    ("InvManagementBacklogEnv", 40000, 3, (75, 9), "next_step", 10),    # horizon = lt_max
+    ("InvManagementBacklogEnv", 40000, 3, (75, 9), "next_step", 7),     # ring slots wrap mid-episode
+    ("InvManagementLostSalesEnv", 40000, 2, (75, 9), "next_step", 25),
 ])
-def test_invmgmt_register_window_rollout_equals_one_wave(gpu, monkeypatch, cls, n, pre, Ks, mode):
+def test_invmgmt_register_window_rollout_equals_one_wave(gpu, monkeypatch, cls, n, pre, Ks, mode, periods):
     """invsim_rollout of the default lead times runs im_roll3_kernel (register
     windows + demand wave); INVSIM_IM_ROLL=0 keeps it on the one-wave kernel.
     Both paths from the same state: identical outputs, demand record and state
-    (wide >= 2^32 orders included)."""
+    (wide >= 2^32 orders included; ring slots of earlier episodes included,
+    over horizons that are and are not multiples of the ring lengths)."""
     import invsim
     envs = []
     for i in range(2):
-        env = getattr(invsim, cls)(n, device=gpu, autoreset_mode=mode, record_demand=True)
+        env = getattr(invsim, cls)(n, device=gpu, autoreset_mode=mode, record_demand=True, periods=periods)
         env.reset(seed=41)
         envs.append(env)
     g = torch.Generator(device=gpu)
@@ -754,7 +758,7 @@ def test_invmgmt_register_window_rollout_equals_one_wave(gpu, monkeypatch, cls, 
             env.step(a)
     for K in Ks:
         a = torch.randint(-5, 260, (K, n, 3), device=gpu, dtype=torch.int64, generator=g)
-        a[:, ::97, 1] = (1 << 32) + 5          # wide requested orders: the int64 side ring
+        a[::2, ::97, 1] = (1 << 32) + 5         # wide requested orders (every other step): the int64 side ring
         outs, dems = [], []
         for i, env in enumerate(envs):
             monkeypatch.setenv("INVSIM_IM_ROLL", "1" if i == 0 else "0")
@@ -930,32 +934,40 @@ def test_net_demand_lookahead_mixed_calls(gpu, graph, kw, monkeypatch):
     same_state()
 
 
-@pytest.mark.parametrize("cls,n", [("InvManagementBacklogEnv", 3000), ("InvManagementLostSalesEnv", 32768)])
-def test_invmgmt_three_role_rollout_equals_two_role(gpu, monkeypatch, cls, n):
+@pytest.mark.parametrize("cls,n,periods", [("InvManagementBacklogEnv", 3000, 30),
+                                           ("InvManagementLostSalesEnv", 32768, 30),
+                                           ("InvManagementBacklogEnv", 3000, 20),
+                                           ("InvManagementBacklogEnv", 3000, 12)])
+def test_invmgmt_three_role_rollout_equals_two_role(gpu, monkeypatch, cls, n, periods):
     """Small batches run im_roll3o_kernel (obs work on a third wave); forcing
     INVSIM_IM_ROLL3O_MAX_N=0 keeps them on im_roll3_kernel.  Same state in:
-    identical outputs, demand record and state out."""
+    identical outputs, demand record and state out.  A last case with the
+    one-wave kernel (INVSIM_IM_ROLL=0) pins both against a slot per step."""
     import invsim
     envs = []
-    for i in range(2):
-        env = getattr(invsim, cls)(n, device=gpu, record_demand=True)
+    for i in range(3):
+        env = getattr(invsim, cls)(n, device=gpu, record_demand=True, periods=periods)
         env.reset(seed=17)
         envs.append(env)
     g = torch.Generator(device=gpu).manual_seed(3)
     for K in (75, 9, 2):
         a = torch.randint(-5, 260, (K, n, 3), device=gpu, dtype=torch.int64, generator=g)
-        a[:, ::89, 2] = (1 << 33) + 1          # wide requested orders
+        a[::3, ::89, 2] = (1 << 33) + 1         # wide requested orders, every third step
         outs, dems = [], []
         for i, env in enumerate(envs):
             if i == 1:
                 monkeypatch.setenv("INVSIM_IM_ROLL3O_MAX_N", "0")
+            if i == 2:
+                monkeypatch.setenv("INVSIM_IM_ROLL", "0")
             outs.append(env.rollout(a))
             dems.append(env._demand.clone())
             monkeypatch.delenv("INVSIM_IM_ROLL3O_MAX_N", raising=False)
-        for x, y in zip(outs[0], outs[1]):
-            assert torch.equal(x, y), K
-        assert torch.equal(dems[0], dems[1])
-        assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
+            monkeypatch.delenv("INVSIM_IM_ROLL", raising=False)
+        for j in (1, 2):
+            for x, y in zip(outs[0], outs[j]):
+                assert torch.equal(x, y), (K, j)
+            assert torch.equal(dems[0], dems[j])
+            assert torch.equal(envs[0].get_state(), envs[j].get_state()), (K, j)
 
 
 @pytest.mark.parametrize("graph,backlog,n,periods,mode", [
