@@ -1179,10 +1179,16 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
 // between barriers c and c + 1 and fills ibuf[c & 1], which the obs wave
 // consumes between barriers c + 1 and c + 2.  Same arithmetic, in the same
 // order, as im_step_regs.
+#ifndef IM_ROLL3O_CH
+#define IM_ROLL3O_CH 4   // swept on MI355X (LostSales 32768 envs): (CH, RD) = (2, 8) 65.6 us, (4, 4) 67.0, (4, 8) 66.5, (8, 4) 74.6
+#endif
+#ifndef IM_ROLL3O_RD
+#define IM_ROLL3O_RD 4
+#endif
 template <int L0, int L1, int L2>
 struct ImLt3o : ImLt3<L0, L1, L2> {
-    static constexpr int CH = 4;                                         // chunk (launch steps)
-    static constexpr int RD = 4;                                         // demand ring depth (chunks)
+    static constexpr int CH = IM_ROLL3O_CH;                              // chunk (launch steps)
+    static constexpr int RD = IM_ROLL3O_RD;                              // demand ring depth (chunks)
     static constexpr int M1 = 3, O = ImLt3<L0, L1, L2>::O;
     static constexpr size_t lds() {
         return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + 2 * CH * M1 * WAVE * 8;
