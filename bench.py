@@ -5,19 +5,26 @@ Default workload (north_star target): InvManagementBacklogEnv, 4 stages,
 the C ABI (libinvsim `invsim_step`), actions pre-generated in HBM (a pool of
 distinct batches cycled per step), outputs into preallocated device buffers,
 NEXT_STEP autoreset (an episode boundary every 31 steps is part of the work).
+The step outputs land in a [32, N] slab that the HIP episode fold
+(`invsim_episode_fold`) reduces to episodic-return statistics every 32 steps
+inside the timed region; one all-reduce of them follows the region.  After
+the step region the same handle runs a timed region of fused K=30 rollouts
+(`invsim_rollout`), reported under "rollout" in the same line.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--mode step|rollout]
 
-Multi-GPU (one process per GPU, torchrun): each rank owns 65 536 envs with
-global seeds rank*65536+i (weak scaling), no collective in the data path;
-barrier + synchronize around the timed region, max time over ranks.  After
-the timed region the per-rank episodic-return statistics are all-reduced over
-RCCL (the only cross-GPU exchange the path has).  --strong splits the
-workload's env count over the ranks instead (strong scaling).
+Multi-GPU (one process per GPU): under torch.distributed.run the ranks come
+from the environment (WORLD_SIZE must equal --gpus); `bench.py --gpus N` run
+directly starts the N ranks itself (torch.distributed.run child, before any
+GPU call) and relays rank 0's line.  Each rank owns 65 536 envs with global
+seeds rank*65536+i (weak scaling), no collective in the data path; barrier +
+synchronize around the timed region, max time over ranks.  --strong splits
+the workload's env count over the ranks instead (strong scaling).
 
-Prints ONE JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per
-launch (SURVEY §8(d) B1 x N) / mean kernel time from HIP events on the stream
-the kernel runs on.  `cpu_baseline` = the C oracle (a single-thread port of the
+Prints ONE JSON line (rank 0).  `roofline.frac` = frac_kernel: algorithmic
+bytes per launch (SURVEY §8(d) B1 x N) / mean launch duration from HIP events
+on the stream the kernel runs on; `frac_wall` beside it uses the wall-clock
+`value` instead.  `cpu_baseline` = the C oracle (a single-thread port of the
 reference step, env loop OpenMP-parallel over up to 16 host cores; the
 single-thread rate beside it) timed on this host on a bounded sample.
 """
@@ -60,6 +67,8 @@ def parse():
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: the workload's env count is the GLOBAL batch, split over ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rollout-line", action="store_true",
+                    help="step mode: skip the K-step rollout region reported under 'rollout'")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--pool", type=int, default=16, help="distinct action batches cycled")
     return ap.parse_args()
@@ -142,19 +151,180 @@ def cpu_baseline(wl, seconds):
                 cpu_model=_cpu_model(), host_cpus_visible=cores)
 
 
+def _spawn_ranks(args):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start N fresh rank
+    processes with torch.distributed.run and relay rank 0's line.  Called
+    before anything touches the GPU; the parent never execs."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return p.wait()
+
+
+def _fold_rows(stats, rew, term, trunc, rows, sp):
+    if rows:
+        stats.update_block(rew[:rows], term[:rows], trunc[:rows], stream=sp)
+
+
+def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
+    """Warm up, then time `steps` env.step()s of the whole batch (mode "step":
+    one invsim_step each; "rollout": invsim_rollout launches of K steps), with
+    barrier + synchronize on both sides and the max over ranks.  The step
+    outputs are written into a [R, N] slab that the HIP episode fold
+    (invsim_episode_fold) reduces every R steps inside the timed region; the
+    statistics are all-reduced once after it."""
+    import torch
+    import invsim
+    from invsim.distributed import EpisodeStats
+    lib, h = env._lib, env._h
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    N, O = env.num_envs, env.obs_dim
+    K = args.rollout_k if mode == "rollout" else 0
+    pool = max(1, args.pool if mode == "step" else 2)
+    acts = make_actions(env, pool, K, gen)
+    ptrs = [a.data_ptr() for a in acts]
+    R = K if K else 32                              # slab rows = steps per fold
+    rew = torch.empty((R, N), dtype=torch.float64, device=dev)
+    term = torch.empty((R, N), dtype=torch.bool, device=dev)
+    trunc = torch.empty((R, N), dtype=torch.bool, device=dev)
+    obs = torch.empty(((K or 1), N, O), dtype=env.obs_dtype, device=dev)
+    po, pr, pt, pu = obs.data_ptr(), rew.data_ptr(), term.data_ptr(), trunc.data_ptr()
+    stats = EpisodeStats(N, dev)
+    if mode == "step":
+        step_fn = lib.invsim_step
+        calls_per_block = R
+
+        def one(i, row):
+            rc = step_fn(h, ptrs[i % pool], po, pr + 8 * row * N, pt + row * N, pu + row * N, None, sp)
+            if rc:
+                raise RuntimeError(invsim._capi.last_error(h))
+        steps_per_call = 1
+    else:
+        fn = lib.invsim_rollout
+        calls_per_block = 1
+
+        def one(i, row):
+            rc = fn(h, K, ptrs[i % pool], po, pr, pt, pu, sp)
+            if rc:
+                raise RuntimeError(invsim._capi.last_error(h))
+        steps_per_call = K
+    rows_per_call = steps_per_call
+
+    calls = max(1, steps // steps_per_call)
+    warm = max(1, warmup // steps_per_call)
+    nblocks = (calls + calls_per_block - 1) // calls_per_block
+    # HIP events on the kernel stream around each block of launches (the fold
+    # runs between blocks, outside the event pairs): sum of the pairs / launches
+    # is the mean launch duration.  torch creates an event at its first record:
+    # record every event once here, so creation stays out of the timed region.
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nblocks)]
+    for a, b in evs:
+        a.record(stream)
+        b.record(stream)
+
+    def region(n_calls, timed):
+        done = 0
+        for bi in range(0, n_calls, calls_per_block):
+            nb = min(calls_per_block, n_calls - bi)
+            if timed:
+                evs[bi // calls_per_block][0].record(stream)
+            for j in range(nb):
+                one(bi + j, j * (rows_per_call if K == 0 else 0))
+            if timed:
+                evs[bi // calls_per_block][1].record(stream)
+            _fold_rows(stats, rew, term, trunc, nb * rows_per_call if K == 0 else K, sp)
+            done += nb
+        return done
+
+    region(warm, False)
+    torch.cuda.synchronize(dev)
+    stats.reset_acc()                  # count the episodes that finish in the timed region
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    region(calls, True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    backend = dist.get_backend() if world > 1 else None
+    cdev = dev if backend == "nccl" else torch.device("cpu")
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ep = stats.allreduce()                                  # RCCL all-reduce of the timed batch's statistics
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / calls
+    total_steps = calls * steps_per_call
+    B = wl["B_io"] + (wl["B_state_rollout"] / K if K else wl["B_state"])
+    achieved = B * N * steps_per_call / (kern_ms * 1e-3) / 1e9
+    achieved_wall = B * N * total_steps / el / 1e9
+    return dict(el=el, calls=calls, warm=warm, steps_per_call=steps_per_call, total_steps=total_steps,
+                N=N, K=K, B=B, kern_ms=kern_ms, achieved=achieved, achieved_wall=achieved_wall, ep=ep)
+
+
+def _roofline(r, traffic, traffic_src):
+    return {"bound": "hbm", "achieved": r["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": r["achieved"] / HBM_PEAK_GBS,
+            "frac_kernel": r["achieved"] / HBM_PEAK_GBS,
+            "frac_wall": r["achieved_wall"] / HBM_PEAK_GBS,
+            "frac_is": "frac_kernel: algorithmic bytes per launch / mean launch duration (HIP events on the "
+                       "kernel stream); frac_wall: value per GPU x bytes_per_env_step / peak (SURVEY 8(d))",
+            "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, calibrated)",
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": r["B"] * r["N"] * r["steps_per_call"],
+            "bytes_per_env_step": r["B"], "kernel_ms_mean": r["kern_ms"],
+            "kernel_timing": "HIP events on the kernel stream around each block of launches / launches"}
+
+
+def _pmc(workload, mode, n_match):
+    """The newest round's PMC summary for this workload and mode
+    (profiles/rNN/pmc_<workload>[_rollout].json, tools/pmc_summary.py)."""
+    import glob
+    suffix = "" if mode == "step" else "_rollout"
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", f"pmc_{workload}{suffix}.json")))
+    if not pmcs or not n_match:
+        return None, None
+    rec = json.load(open(pmcs[-1]))
+    return rec["hbm_bytes_per_launch"], os.path.relpath(pmcs[-1], ROOT)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _spawn_ranks(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # RCCL ("nccl") over xGMI; INVSIM_BENCH_BACKEND=gloo rehearses the multi-rank
-    # path with several ranks on one GPU (RCCL refuses two ranks per device)
+    # RCCL ("nccl") over xGMI, one rank per GPU; INVSIM_BENCH_BACKEND=gloo
+    # rehearses the multi-rank path with several ranks on one GPU
     backend = os.environ.get("INVSIM_BENCH_BACKEND", "nccl")
     if world > 1:
-        local = local % torch.cuda.device_count()
+        ndev = torch.cuda.device_count()
+        if backend == "nccl":
+            if local >= ndev:
+                raise RuntimeError(f"bench.py: LOCAL_RANK {local} but only {ndev} GPUs visible (RCCL needs one GPU per rank)")
+        else:
+            local = local % ndev
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -171,140 +341,50 @@ def main():
     env = getattr(invsim, wl["cls"])(n, device=dev, global_offset=rank * n, copy=False)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
-    K = args.rollout_k if args.mode == "rollout" else 0
-    pool = max(1, args.pool if args.mode == "step" else 2)
-    acts = make_actions(env, pool, K, gen)
     env.reset(seed=0)
-    lib, h = env._lib, env._h
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
-    N, O = env.num_envs, env.obs_dim
-    if args.mode == "step":
-        obs = torch.empty((N, O), dtype=env.obs_dtype, device=dev)
-        rew = torch.empty(N, dtype=torch.float64, device=dev)
-        term = torch.empty(N, dtype=torch.bool, device=dev)
-        trunc = torch.empty(N, dtype=torch.bool, device=dev)
-        ptrs = [a.data_ptr() for a in acts]
-        po, pr, pt, pu = obs.data_ptr(), rew.data_ptr(), term.data_ptr(), trunc.data_ptr()
-        step_fn = lib.invsim_step
-
-        def one(i):
-            rc = step_fn(h, ptrs[i % pool], po, pr, pt, pu, None, sp)
-            if rc:
-                raise RuntimeError(invsim._capi.last_error(h))
-        steps_per_call = 1
-    else:
-        obs = torch.empty((K, N, O), dtype=env.obs_dtype, device=dev)
-        rew = torch.empty((K, N), dtype=torch.float64, device=dev)
-        term = torch.empty((K, N), dtype=torch.bool, device=dev)
-        trunc = torch.empty((K, N), dtype=torch.bool, device=dev)
-        ptrs = [a.data_ptr() for a in acts]
-        po, pr, pt, pu = obs.data_ptr(), rew.data_ptr(), term.data_ptr(), trunc.data_ptr()
-        fn = lib.invsim_rollout
-
-        def one(i):
-            rc = fn(h, K, ptrs[i % pool], po, pr, pt, pu, sp)
-            if rc:
-                raise RuntimeError(invsim._capi.last_error(h))
-        steps_per_call = K
-
-    calls = max(1, args.steps // steps_per_call)
-    warm = max(1, args.warmup // steps_per_call)
-    # HIP events on the stream the kernels run on, around the timed region:
-    # launches are back to back there, so (end - start) / calls is the mean
-    # kernel duration (+ inter-kernel gaps, ~0 on a saturated queue).  torch
-    # creates the HIP event at its first record: record both once here so the
-    # creation stays out of the timed region (~10 us of wall time per region,
-    # tools/sync_overhead.py)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for i in range(warm):
-        one(i)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(calls):
-        one(i)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    # collectives on device tensors over RCCL; gloo (rehearsal) reduces host copies
-    cdev = dev if backend == "nccl" else torch.device("cpu")
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    total_steps = calls * steps_per_call  # env.step() calls over the batch
-    env_steps = total_steps * N * world
-    kern_ms_mean = ev0.elapsed_time(ev1) / calls
-
-    # episodic-return statistics all-reduced across GPUs (RCCL): one short episode
-    env2 = getattr(invsim, wl["cls"])(min(N, 4096), device=dev, global_offset=rank * N)
-    env2.reset(seed=0)
-    a2 = make_actions(env2, 1, 0, gen)[0]
-    ret = torch.zeros(env2.num_envs, dtype=torch.float64, device=dev)
-    while True:
-        _, r, _, tr, _ = env2.step(a2)
-        ret += r
-        if bool(tr.all()):
-            break
-    stats = torch.stack([ret.sum(), (ret * ret).sum(),
-                         torch.tensor(float(env2.num_envs), dtype=torch.float64, device=dev)])
-    if world > 1:
-        stats = stats.to(cdev)
-        dist.all_reduce(stats)
-    stats = stats.cpu().tolist()
-
-    B = wl["B_io"] + (wl["B_state_rollout"] / K if K else wl["B_state"])
-    achieved = B * N * steps_per_call / (kern_ms_mean * 1e-3) / 1e9
-    traffic, traffic_src = None, None
-    # the newest round's PMC summary (profiles/rNN/pmc_<workload>.json, tools/pmc_summary.py)
-    import glob
-    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", f"pmc_{args.workload}.json")))
-    pmc = pmcs[-1] if pmcs else ""
-    if pmc and args.mode == "step" and N == wl["n"]:
-        rec = json.load(open(pmc))
-        traffic, traffic_src = rec["hbm_bytes_per_launch"], os.path.relpath(pmc, ROOT)
+    r = run_region(args, env, wl, args.mode, args.steps, args.warmup, world, dev, gen, dist)
+    full = n == wl["n"] and not args.strong
+    traffic, traffic_src = _pmc(args.workload, args.mode, full)
+    N = r["N"]
     out = {
         "metric": "env-steps/sec (batched) at 1/2/4/8 MI355X; % HBM roofline",
-        "value": env_steps / el,
+        "value": r["total_steps"] * N * world / r["el"],
         "unit": "env-steps/s",
         "n_gpus": world,
-        "steps": total_steps,
-        "warmup": warm * steps_per_call,
-        "ms_per_step": el * 1e3 / total_steps,
+        "ranks": dist.get_world_size() if world > 1 else 1,
+        "steps": r["total_steps"],
+        "warmup": r["warm"] * r["steps_per_call"],
+        "ms_per_step": r["el"] * 1e3 / r["total_steps"],
         "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": wl["dtype"],
         "data": "synthetic (pre-generated random actions in HBM, seeds 0..N-1 per global env index)",
         "config": {"workload": wl["desc"], "envs_per_gpu": N, "global_envs": N * world,
-                   "mode": args.mode + (f" K={K}" if K else ""), "autoreset": "next_step",
+                   "mode": args.mode + (f" K={r['K']}" if r["K"] else ""), "autoreset": "next_step",
                    "parallelism": f"dp{world} (env sharding, no data-path collective)",
-                   "backend": backend if world > 1 else None},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, calibrated)",
-                     "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": B * N * steps_per_call,
-                     "bytes_per_env_step": B, "kernel_ms_mean": kern_ms_mean,
-                     "kernel_timing": "HIP events on the kernel stream around the timed region / launches"},
-        "episode_stats": {"sum_return": stats[0], "sum_sq_return": stats[1], "episodes": stats[2]},
+                   "backend": (backend if world > 1 else None)},
+        "roofline": _roofline(r, traffic, traffic_src),
+        "episode_stats": dict(r["ep"], source="timed batch: HIP episode fold of the timed steps' rewards and "
+                                              "done flags, one all-reduce after the region"),
     }
+    if args.mode == "step" and not args.no_rollout_line:
+        # the fused K-step rollout of the same handle, timed the same way
+        rr = run_region(args, env, wl, "rollout", max(args.steps, 10 * args.rollout_k),
+                        2 * args.rollout_k, world, dev, gen, dist)
+        t2, s2 = _pmc(args.workload, "rollout", full)
+        out["rollout"] = {"value": rr["total_steps"] * N * world / rr["el"], "unit": "env-steps/s",
+                          "steps": rr["total_steps"], "launches": rr["calls"], "K": rr["K"],
+                          "ms_per_launch": rr["el"] * 1e3 / rr["calls"],
+                          "roofline": _roofline(rr, t2, s2)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

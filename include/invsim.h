@@ -229,6 +229,27 @@ int invsim_metrics_dim(const invsim_handle *h, int32_t *dim);
 int invsim_rollout_policy(invsim_handle *h, int32_t K, const invsim_policy *policy, void *obs, double *reward,
                           uint8_t *terminated, uint8_t *truncated, void *actions, double *metrics, void *stream);
 
+/* Episodic-return statistics of K steps of outputs, the reduction the
+ * reference's evaluation harness keeps per episode (episode_rewards ->
+ * mean/std, benchmark_InvManagementBacklogEnv.py:389-440).  Handle-free:
+ * reward [K][n_envs] f64; terminated / truncated [K][n_envs] u8 (either may be
+ * NULL); ret [n_envs] f64 running per-env return (in/out); acc [4] f64 (+=):
+ * sum of finished-episode returns, sum of their squares, finished episodes,
+ * sum of every reward folded.  Device pointers; the stream's device runs it.
+ * invsim.distributed.EpisodeStats all-reduces acc over RCCL. */
+int invsim_episode_fold(const double *reward, const uint8_t *terminated, const uint8_t *truncated, int32_t K,
+                        int64_t n_envs, double *ret, double *acc, void *stream);
+
+/* Debug builds only (make -C csrc ptrs_stats -> invsim/_lib/debug/): PTRS
+ * log-acceptance statistics since the last clear, summed over kernels:
+ * out[0] log tests, out[1] tests the f64 fallback decided, out[2] bit pattern
+ * of the smallest relative margin |lhs - rhs| / (sum of |terms|) (f64),
+ * out[3] f32-decided tests that disagree with the f64 test.  Synchronises the
+ * device.  The product build returns INVSIM_EINVAL.  (No reference
+ * equivalent: evidence for the numpy random_poisson_ptrs restatement,
+ * distributions.c, SURVEY App. B.) */
+int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear);
+
 /* Which kernel a handle runs: 0 = the generic kernel of its family, 1 / 2 =
  * NetInvMgmt specialised at compile time for the reference's default /
  * custom supply network (chosen at create when the graph equals one of them). */

@@ -1,5 +1,6 @@
 // C ABI of libinvsim (include/invsim.h): handle lifetime, HBM state arena,
 // spec validation (the reference's assert checks), and kernel launches.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -12,8 +13,6 @@
 
 #include "../../include/invsim.h"
 #include "kernels.hpp"
-
-#include <rocprofiler-sdk-roctx/roctx.h>
 
 using namespace invsim;
 
@@ -33,6 +32,12 @@ struct Field {
 
 namespace invsim {
 int net_spec_match(const invsim_netinvmgmt_spec &h);   // netspec.hip
+#ifdef INVSIM_PTRS_STATS
+hipError_t ptrs_stats_nv(unsigned long long *out, bool clear);
+hipError_t ptrs_stats_im(unsigned long long *out, bool clear);
+hipError_t ptrs_stats_netspec(unsigned long long *out, bool clear);
+hipError_t ptrs_stats_net(unsigned long long *out, bool clear);
+#endif
 }
 
 struct invsim_handle {
@@ -66,10 +71,33 @@ namespace {
 
 // roctx range around an ABI call (SURVEY §5 tracing: step / rollout / reset
 // show up as named ranges under `rocprofv3 --marker-trace`; a no-op call when
-// no profiler is attached)
+// no profiler is attached).  roctx is opened with dlopen at the first call, so
+// libinvsim.so has no load-time dependency on it; without it ranges are no-ops.
+struct Roctx {
+    int (*push)(const char *) = nullptr;
+    int (*pop)() = nullptr;
+    Roctx() {
+        void *so = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!so) so = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!so) return;
+        push = reinterpret_cast<int (*)(const char *)>(dlsym(so, "roctxRangePushA"));
+        pop = reinterpret_cast<int (*)()>(dlsym(so, "roctxRangePop"));
+        if (!push || !pop) push = nullptr, pop = nullptr;
+    }
+};
+
+const Roctx &roctx() {
+    static const Roctx r;
+    return r;
+}
+
 struct TraceRange {
-    explicit TraceRange(const char *name) { roctxRangePushA(name); }
-    ~TraceRange() { roctxRangePop(); }
+    explicit TraceRange(const char *name) {
+        if (roctx().push) roctx().push(name);
+    }
+    ~TraceRange() {
+        if (roctx().pop) roctx().pop();
+    }
 };
 
 struct DeviceGuard {
@@ -884,6 +912,39 @@ int invsim_rollout_policy(invsim_handle *h, int32_t K, const invsim_policy *poli
     }
     DeviceGuard g(h->device);
     return run_steps(h, K, nullptr, obs, reward, terminated, truncated, nullptr, (hipStream_t)stream, &p);
+}
+
+int invsim_episode_fold(const double *reward, const uint8_t *terminated, const uint8_t *truncated, int32_t K,
+                        int64_t n_envs, double *ret, double *acc, void *stream) {
+    TraceRange tr_("invsim_episode_fold");
+    if (!reward || !ret || !acc || K < 0 || n_envs < 0)
+        return fail(nullptr, INVSIM_EINVAL, "episode_fold: null buffer or negative size");
+    hipError_t e = episode_fold_launch(reward, terminated, truncated, K, n_envs, ret, acc, (hipStream_t)stream);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(nullptr, e, "episode_fold launch");
+}
+
+int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear) {
+    if (!out) return fail(nullptr, INVSIM_EINVAL, "null argument");
+#ifdef INVSIM_PTRS_STATS
+    hipError_t (*tus[4])(unsigned long long *, bool) = {ptrs_stats_nv, ptrs_stats_im, ptrs_stats_netspec,
+                                                        ptrs_stats_net};
+    out[0] = out[1] = out[3] = 0;
+    out[2] = 0x7ff0000000000000ull;
+    for (auto f : tus) {
+        unsigned long long v[4];
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess) e = f(v, clear != 0);
+        if (e != hipSuccess) return hip_fail(nullptr, e, "ptrs stats");
+        out[0] += v[0];
+        out[1] += v[1];
+        out[3] += v[3];
+        out[2] = std::min<uint64_t>(out[2], v[2]);
+    }
+    return INVSIM_OK;
+#else
+    (void)clear;
+    return fail(nullptr, INVSIM_EINVAL, "not a PTRS-statistics build (make -C csrc ptrs_stats)");
+#endif
 }
 
 int invsim_kernel_variant(const invsim_handle *h, int32_t *variant) {

@@ -44,7 +44,66 @@ __global__ void __launch_bounds__(256) period_fill_kernel(Common cm, int32_t t) 
     if (e < cm.N) cm.period[e] = t;
 }
 
+// Episodic-return reduction of K steps of outputs (the statistics the
+// reference's harness keeps per episode, benchmark_InvManagementBacklogEnv.py:
+// 389-440): per env, ret += reward[k]; at a terminated|truncated step the return
+// is folded into acc = [sum, sum of squares, episodes] and restarts at 0.  acc[3]
+// sums every folded reward.  One lane per env walks its K rows (each row a
+// coalesced 8-B / 1-B stream); the workgroup reduces in registers + LDS and
+// adds its four partials to acc with vector f64 atomics.
+__global__ void __launch_bounds__(256)
+episode_fold_kernel(const double *rew, const uint8_t *term, const uint8_t *trunc, int32_t K, int64_t N,
+                    double *ret, double *acc) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double s = 0.0, s2 = 0.0, c = 0.0, all = 0.0;
+    if (e < N) {
+        double r = ret[e];
+        for (int k = 0; k < K; ++k) {
+            const int64_t i = (int64_t)k * N + e;
+            const double x = rew[i];
+            r += x;
+            all += x;
+            const bool d = (term && term[i]) || (trunc && trunc[i]);
+            if (d) {
+                s += r;
+                s2 += r * r;
+                c += 1.0;
+                r = 0.0;
+            }
+        }
+        ret[e] = r;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        s += __shfl_xor(s, off);
+        s2 += __shfl_xor(s2, off);
+        c += __shfl_xor(c, off);
+        all += __shfl_xor(all, off);
+    }
+    __shared__ double part[4][4];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) {
+        part[w][0] = s;
+        part[w][1] = s2;
+        part[w][2] = c;
+        part[w][3] = all;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const int j = threadIdx.x;
+        const double v = part[0][j] + part[1][j] + part[2][j] + part[3][j];
+        atomicAdd(&acc[j], v);
+    }
+}
+
 static inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t episode_fold_launch(const double *rew, const uint8_t *term, const uint8_t *trunc, int32_t K,
+                               int64_t N, double *ret, double *acc, hipStream_t s) {
+    if (N == 0) return hipSuccess;
+    hipLaunchKernelGGL(episode_fold_kernel, dim3(grid_for(N, 256)), dim3(256), 0, s, rew, term, trunc, K, N,
+                       ret, acc);
+    return hipGetLastError();
+}
 
 hipError_t seed_range_launch(const Common &cm, uint64_t base_lo, uint64_t base_hi, int64_t first,
                              const uint8_t *mask, hipStream_t s) {

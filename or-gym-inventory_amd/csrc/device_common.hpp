@@ -163,7 +163,43 @@ __device__ __forceinline__ double ptrs_rhs(const PtrsConst &c, const double *rhs
 // decided with the f32 hardware log2 (v_log_f32) whenever the f32 estimate is
 // farther from r than a rigorous bound on its error; only near-ties (and
 // overflow) evaluate the f64 logs.  Same decision as the f64 test.
+#ifdef INVSIM_PTRS_STATS
+// Debug build only (make ptrs_stats): per translation unit, [0] log tests,
+// [1] tests decided by the f64 fallback, [2] bits of the smallest relative
+// margin |lhs - r| / (|log V| + |log(1/alpha)| + |log x| + |r|) over all tests
+// (non-negative doubles order like their bit patterns), [3] f32 decisions that
+// disagree with the f64 test (must stay 0).  Read by invsim_debug_ptrs_stats.
+static __device__ unsigned long long g_ptrs_stats[4] = {0ull, 0ull, 0x7ff0000000000000ull, 0ull};
+#define INVSIM_PTRS_STATS_TU(tu)                                                                   \
+    hipError_t ptrs_stats_##tu(unsigned long long *out, bool clear) {                              \
+        hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptrs_stats), sizeof(g_ptrs_stats));   \
+        if (e != hipSuccess || !clear) return e;                                                   \
+        const unsigned long long init[4] = {0ull, 0ull, 0x7ff0000000000000ull, 0ull};              \
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_ptrs_stats), init, sizeof(init));                    \
+    }
+
+__device__ __forceinline__ bool ptrs_log_accept_f32(const PtrsConst &c, double V, double us, double r, bool &decided);
+
 __device__ __forceinline__ bool ptrs_log_accept(const PtrsConst &c, double V, double us, double r) {
+    bool decided;
+    const bool fast = ptrs_log_accept_f32(c, V, us, r, decided);
+    const double lv = log(V), lx = log(c.a / (us * us) + c.b);
+    const double lhs = lv + c.log_invalpha - lx;
+    const bool exact = lhs <= r;
+    const double margin = fabs(lhs - r) / (fabs(lv) + fabs(c.log_invalpha) + fabs(lx) + fabs(r));
+    atomicAdd(&g_ptrs_stats[0], 1ull);
+    if (!decided) atomicAdd(&g_ptrs_stats[1], 1ull);
+    if (decided && fast != exact) atomicAdd(&g_ptrs_stats[3], 1ull);
+    atomicMin(&g_ptrs_stats[2], (unsigned long long)__double_as_longlong(margin));
+    return exact;
+}
+
+__device__ __forceinline__ bool ptrs_log_accept_f32(const PtrsConst &c, double V, double us, double r, bool &decided) {
+    decided = true;
+#else
+#define INVSIM_PTRS_STATS_TU(tu)
+__device__ __forceinline__ bool ptrs_log_accept(const PtrsConst &c, double V, double us, double r) {
+#endif
     constexpr double LN2 = 0.69314718055994530942;
     const float us32 = (float)us;
     const float x32 = (float)c.a / (us32 * us32) + (float)c.b;   // rel. error < 8 * 2^-24
@@ -178,6 +214,9 @@ __device__ __forceinline__ bool ptrs_log_accept(const PtrsConst &c, double V, do
         if (lhs + err < r) return true;
         if (lhs - err > r) return false;
     }
+#ifdef INVSIM_PTRS_STATS
+    decided = false;
+#endif
     return (log(V) + c.log_invalpha - log(c.a / (us * us) + c.b)) <= r;
 }
 

@@ -1180,10 +1180,10 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
 // consumes between barriers c + 1 and c + 2.  Same arithmetic, in the same
 // order, as im_step_regs.
 #ifndef IM_ROLL3O_CH
-#define IM_ROLL3O_CH 4   // swept on MI355X (LostSales 32768 envs): (CH, RD) = (2, 8) 65.6 us, (4, 4) 67.0, (4, 8) 66.5, (8, 4) 74.6
+#define IM_ROLL3O_CH 2   // swept on MI355X (LostSales 32768 envs): (CH, RD) = (2, 8) 65.6 us, (4, 4) 67.0, (4, 8) 66.5, (8, 4) 74.6
 #endif
 #ifndef IM_ROLL3O_RD
-#define IM_ROLL3O_RD 4
+#define IM_ROLL3O_RD 8
 #endif
 template <int L0, int L1, int L2>
 struct ImLt3o : ImLt3<L0, L1, L2> {
@@ -1627,6 +1627,8 @@ hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_
 #undef L_
     return hipGetLastError();
 }
+
+INVSIM_PTRS_STATS_TU(im)
 
 }  // namespace invsim
 

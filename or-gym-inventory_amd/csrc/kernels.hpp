@@ -352,6 +352,8 @@ hipError_t seed_range_launch(const Common &cm, uint64_t base_lo, uint64_t base_h
 hipError_t seed_words_launch(const Common &cm, const uint32_t *words, const int32_t *nwords,
                              const uint8_t *mask, hipStream_t s);
 hipError_t period_fill_launch(const Common &cm, int32_t t, hipStream_t s);
+hipError_t episode_fold_launch(const double *rew, const uint8_t *term, const uint8_t *trunc, int32_t K,
+                               int64_t N, double *ret, double *acc, hipStream_t s);
 
 hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, hipStream_t s);
 // ahead / slot: the demand lookahead cache state, as for im_run_launch

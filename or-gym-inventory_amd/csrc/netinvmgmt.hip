@@ -360,4 +360,6 @@ hipError_t net_reset_launch(const NetParams &p, const uint8_t *mask, float *obs,
     return hipGetLastError();
 }
 
+INVSIM_PTRS_STATS_TU(net)
+
 }  // namespace invsim

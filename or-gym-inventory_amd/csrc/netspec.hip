@@ -1451,4 +1451,6 @@ hipError_t net_spec_launch(int which, const NetParams &p, int t_u, const PolicyI
     }
 }
 
+INVSIM_PTRS_STATS_TU(netspec)
+
 }  // namespace invsim

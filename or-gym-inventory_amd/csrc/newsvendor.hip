@@ -1221,6 +1221,8 @@ hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, h
     return hipGetLastError();
 }
 
+INVSIM_PTRS_STATS_TU(nv)
+
 }  // namespace invsim
 
 #ifdef INVSIM_TIMING

@@ -25,7 +25,8 @@ EXPORTS = (
     "invsim_step", "invsim_rollout", "invsim_status", "invsim_kernel_variant", "invsim_metrics_dim",
     "invsim_rollout_policy", "invsim_info_record_dim", "invsim_set_info_record", "invsim_set_info_demand",
     "invsim_state_bytes",
-    "invsim_state_field", "invsim_get_state", "invsim_set_state",
+    "invsim_state_field", "invsim_get_state", "invsim_set_state", "invsim_episode_fold",
+    "invsim_debug_ptrs_stats",
 )
 
 
@@ -99,6 +100,8 @@ def _declare(lib):
         "invsim_state_field": ([H, I32, P, P, P, P, P], C.c_int),
         "invsim_get_state": ([H, P, P], C.c_int),
         "invsim_set_state": ([H, P, P], C.c_int),
+        "invsim_episode_fold": ([P, P, P, I32, I64, P, P, P], C.c_int),
+        "invsim_debug_ptrs_stats": ([P, I32], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -6,8 +6,8 @@ with ``seed + offset + i`` (``global_offset`` of the VectorEnv), which makes
 every env's trajectory identical for any W.  The only collective is the
 episodic-return reduction the harness reports (mean / std / count of episode
 returns, ``benchmark_InvManagementBacklogEnv.py:389-440``): ONE all-reduce of
-three f64 per episode boundary over RCCL (torch.distributed "nccl" backend on
-ROCm), latency-bound at 24 bytes.
+four f64 over RCCL (torch.distributed "nccl" backend on ROCm), latency-bound
+at 32 bytes.
 """
 import torch
 import torch.distributed as dist
@@ -24,26 +24,69 @@ def shard_range(global_envs, rank, world):
 
 
 class EpisodeStats:
-    """Accumulates per-env returns on device; folds finished episodes into
-    [sum, sum of squares, count] and all-reduces them across ranks."""
+    """Accumulates per-env returns; folds finished episodes into
+    acc = [sum, sum of squares, episodes, sum of all rewards] and all-reduces
+    acc across ranks.
+
+    Device tensors are folded by the HIP kernel ``invsim_episode_fold`` (one
+    launch per block of K steps, reading the step outputs where the env wrote
+    them).  Host tensors (a CPU rehearsal stepping the oracle) are folded with
+    the same arithmetic in torch: there is no device data to hand the kernel.
+    """
 
     def __init__(self, num_envs, device):
-        self.ret = torch.zeros(num_envs, dtype=torch.float64, device=device)
-        self.acc = torch.zeros(3, dtype=torch.float64, device=device)
+        self.device = torch.device(device)
+        self.num_envs = int(num_envs)
+        self.ret = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self.acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+
+    def reset_acc(self):
+        """Forget the folded episodes; running returns carry on."""
+        self.acc.zero_()
 
     def update(self, reward, done):
         """reward [N] f64, done [N] bool (terminated | truncated) of one step."""
-        self.ret += reward
-        d = done.to(torch.float64)
-        r = self.ret * d
-        self.acc += torch.stack([r.sum(), (r * r).sum(), d.sum()])
-        self.ret *= (1.0 - d)
+        self.update_block(reward.reshape(1, -1), None, done.reshape(1, -1))
+
+    def update_block(self, reward, terminated=None, truncated=None, stream=None):
+        """reward [K, N] f64; terminated / truncated [K, N] bool (either may be
+        None) of K consecutive steps."""
+        K, N = reward.shape
+        if N != self.num_envs:
+            raise ValueError(f"EpisodeStats: {N} envs, expected {self.num_envs}")
+        flags = [f for f in (terminated, truncated) if f is not None]
+        if self.device.type == "cuda":
+            from . import _capi
+            for f in [reward] + flags:
+                if f.device != self.device or not f.is_contiguous() or f.shape != (K, N):
+                    raise ValueError("EpisodeStats: outputs must be contiguous [K, N] tensors on the stats device")
+            if reward.dtype != torch.float64 or any(f.dtype not in (torch.bool, torch.uint8) for f in flags):
+                raise TypeError("EpisodeStats: reward f64, flags bool/uint8")
+            if stream is None:
+                stream = torch._C._cuda_getCurrentRawStream(self.device.index)
+            ptr = (lambda t: t.data_ptr() if t is not None else None)
+            _capi.check(_capi.lib().invsim_episode_fold(
+                reward.data_ptr(), ptr(terminated), ptr(truncated), K, N, self.ret.data_ptr(),
+                self.acc.data_ptr(), stream), None, "invsim_episode_fold")
+            return
+        done = torch.zeros((K, N), dtype=torch.bool)
+        for f in flags:
+            done |= f.to(torch.bool)
+        for k in range(K):
+            self.ret += reward[k]
+            d = done[k].to(torch.float64)
+            r = self.ret * d
+            self.acc += torch.stack([r.sum(), (r * r).sum(), d.sum(), reward[k].sum()])
+            self.ret *= (1.0 - d)
 
     def allreduce(self, group=None):
         out = self.acc.clone()
         if dist.is_available() and dist.is_initialized():
+            if dist.get_backend(group) == "gloo" and out.is_cuda:
+                out = out.cpu()
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
-        s, s2, n = out.tolist()
+        s, s2, n, tot = out.tolist()
         mean = s / n if n else float("nan")
         var = max(s2 / n - mean * mean, 0.0) if n else float("nan")
-        return {"episodes": n, "mean_return": mean, "std_return": var ** 0.5, "sum": s, "sum_sq": s2}
+        return {"episodes": n, "mean_return": mean, "std_return": var ** 0.5, "sum": s, "sum_sq": s2,
+                "reward_sum": tot}

@@ -1087,3 +1087,22 @@ void orc_net_step(void *p, const float *action, float *obs, double *reward, uint
         if (Po) for (int j = 0; j < J; j++) Po[(int64_t)i * J + j] = prof[j];
     }
 }
+
+/* ======================================================================
+ * Generator states (test access: the final PCG64 state of every stream is
+ * compared with the device's after long runs)
+ * ==================================================================== */
+void orc_nv_rng(void *p, uint64_t *out /*[n][4]*/) {
+    nv_t *h = (nv_t *)p;
+    memcpy(out, h->rng, sizeof(uint64_t) * 4 * (size_t)h->n);
+}
+
+void orc_im_rng(void *p, uint64_t *out) {
+    im_t *h = (im_t *)p;
+    memcpy(out, h->rng, sizeof(uint64_t) * 4 * (size_t)h->n);
+}
+
+void orc_net_rng(void *p, uint64_t *out) {
+    net_t *h = (net_t *)p;
+    memcpy(out, h->rng, sizeof(uint64_t) * 4 * (size_t)h->n);
+}

@@ -60,6 +60,7 @@ def _lib():
         getattr(lib, f"orc_{fam}_destroy").argtypes = [P]
         getattr(lib, f"orc_{fam}_seed").argtypes = [P, P, P]
         getattr(lib, f"orc_{fam}_reset").argtypes = [P, P]
+        getattr(lib, f"orc_{fam}_rng").argtypes = [P, P]
     lib.orc_nv_step.argtypes = [P] * 6
     lib.orc_nv_get_params.argtypes = [P, P]
     lib.orc_im_step.argtypes = [P] * 10
@@ -183,6 +184,41 @@ class _Base:
         w, nw = seed_words(seeds)
         assert len(w) == self.n
         getattr(lib(), f"orc_{self.fam}_seed")(self.h, _p(w), _p(nw))
+
+    def rng_state(self):
+        """[n][4] uint64 (state hi, state lo, inc hi, inc lo) of every env's PCG64."""
+        out = np.zeros((self.n, 4), np.uint64)
+        getattr(lib(), f"orc_{self.fam}_rng")(self.h, _p(out))
+        return out
+
+    _NULLS = {"nv": 1, "im": 5, "net": 7}
+
+    def run_returns(self, action_pool, T, ret=None):
+        """T steps under NEXT_STEP autoreset (the call after a truncation is a
+        reset: reward 0, no step), call k taking action_pool[k % P], without
+        observations.  Returns (per-env sum of rewards added in call order,
+        f64; truncations seen).  The env must be freshly reset."""
+        n = self.n
+        pool = [np.ascontiguousarray(a) for a in action_pool]
+        rew = np.zeros(n, np.float64)
+        tr = np.zeros(n, np.uint8)
+        ret = np.zeros(n, np.float64) if ret is None else ret
+        zero = np.zeros(n, np.float64)
+        f = getattr(lib(), f"orc_{self.fam}_step")
+        nulls = [None] * self._NULLS[self.fam]
+        pending, ntr = False, 0
+        for k in range(T):
+            if pending:
+                getattr(lib(), f"orc_{self.fam}_reset")(self.h, None)
+                ret += zero
+                pending = False
+                continue
+            f(self.h, _p(pool[k % len(pool)]), None, _p(rew), _p(tr), *nulls)
+            ret += rew
+            if tr.any():
+                assert tr.all(), "lock-step episodes"
+                pending, ntr = True, ntr + 1
+        return ret, ntr
 
 
 # ---------------------------------------------------------------- Newsvendor

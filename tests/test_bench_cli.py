@@ -1,0 +1,54 @@
+"""CPU checks of bench.py's launcher contract and of the episodic-return fold's
+host arithmetic (the HIP fold is checked in tests/test_gpu_episode_fold.py)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_refuses_world_size_mismatch():
+    """under a launcher whose WORLD_SIZE differs from --gpus, bench.py exits
+    non-zero before touching a GPU (no silent single-rank timing)"""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "8"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2
+    assert "WORLD_SIZE=1" in p.stderr
+
+
+def _numpy_fold(rew, done, ret0):
+    ret = ret0.copy()
+    s = s2 = c = 0.0
+    for k in range(rew.shape[0]):
+        ret += rew[k]
+        d = done[k]
+        s += ret[d].sum()
+        s2 += (ret[d] ** 2).sum()
+        c += d.sum()
+        ret[d] = 0.0
+    return ret, np.array([s, s2, c, rew.sum()])
+
+
+def test_episode_stats_block_fold_host():
+    from invsim.distributed import EpisodeStats
+    rng = np.random.default_rng(5)
+    K, N = 37, 513
+    st = EpisodeStats(N, "cpu")
+    ret0 = np.zeros(N)
+    acc = np.zeros(4)
+    for _ in range(3):
+        rew = rng.normal(size=(K, N)) * 100
+        term = rng.random((K, N)) < 0.03
+        trunc = rng.random((K, N)) < 0.05
+        st.update_block(torch.from_numpy(rew), torch.from_numpy(term), torch.from_numpy(trunc))
+        ret0, a = _numpy_fold(rew, term | trunc, ret0)
+        acc += a
+    assert np.allclose(st.ret.numpy(), ret0, rtol=1e-12, atol=1e-9)
+    assert np.allclose(st.acc.numpy(), acc, rtol=1e-12)
+    res = st.allreduce()
+    assert res["episodes"] == acc[2] and res["reward_sum"] == pytest.approx(acc[3])

@@ -47,21 +47,66 @@ def test_bench_single_gpu_line():
     assert p.returncode == 0, p.stderr[-2000:]
     d = _last_json(p.stdout)
     _check_line(d, 1, 20, 5)
+    assert d["ranks"] == 1
     assert d["config"]["envs_per_gpu"] == 65536
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    # the fused rollout region of the same handle rides along
+    ro = d["rollout"]
+    assert ro["K"] == 30 and ro["steps"] == 300 and ro["value"] > 0
+    assert 0 < ro["roofline"]["frac"] < 1.5
+    # timed steps 5..24: no episode ends, every reward of the region is folded
+    ep = d["episode_stats"]
+    assert ep["episodes"] == 0 and ep["reward_sum"] != 0
+
+
+def test_bench_episode_stats_from_timed_batch():
+    """steps 5..66 contain two truncations per env (periods 30, 61 of the
+    31-call NEXT_STEP cycle): the fold counts exactly 2 N episodes."""
+    p = subprocess.run([sys.executable, "bench.py", "--steps", "62", "--warmup", "5", "--no-cpu-baseline",
+                        "--no-rollout-line", "--n-envs", "4096"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _last_json(p.stdout)
+    assert d["episode_stats"]["episodes"] == 2 * 4096
+    assert d["episode_stats"]["mean_return"] == d["episode_stats"]["mean_return"]   # not NaN
 
 
 def test_bench_two_ranks_gloo_rehearsal():
     env = dict(os.environ, INVSIM_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5", "--n-envs", "8192"]
+           "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5", "--n-envs", "8192", "--no-rollout-line"]
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     d = _last_json(p.stdout)
     _check_line(d, 2, 20, 5)
     assert d["config"]["backend"] == "gloo"
     assert "cpu_baseline" not in d                      # rank 0 at N=1 only
-    # the statistics all-reduce summed both ranks' episodes
-    assert d["episode_stats"]["episodes"] == 2 * 4096
+    assert d["ranks"] == 2
+
+
+def _bench_spawned(extra):
+    """plain `bench.py --gpus 2` (no torchrun around it): bench.py starts the ranks"""
+    env = dict(os.environ, INVSIM_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--warmup", "5", "--no-rollout-line"] + extra
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return _last_json(p.stdout)
+
+
+def test_bench_gpus_flag_starts_ranks_weak():
+    d = _bench_spawned(["--steps", "62", "--n-envs", "8192"])
+    _check_line(d, 2, 62, 5)
+    assert d["ranks"] == 2 and d["config"]["backend"] == "gloo" and d["scaling"] == "weak"
+    assert d["config"]["envs_per_gpu"] == 8192 and d["config"]["global_envs"] == 2 * 8192
+    # the statistics all-reduce summed both ranks' episodes of the timed batch
+    assert d["episode_stats"]["episodes"] == 2 * 2 * 8192
+
+
+def test_bench_gpus_flag_strong_net():
+    d = _bench_spawned(["--steps", "20", "--workload", "net_backlog", "--strong"])
+    _check_line(d, 2, 20, 5)
+    assert d["scaling"] == "strong" and d["ranks"] == 2
+    assert d["config"]["envs_per_gpu"] == 16384 and d["config"]["global_envs"] == 32768

@@ -58,7 +58,8 @@ def run_stream_loop(K, CH, RD, RL, nb, t0, T, accept, lanes=64):
     (30, 2, 8, 1, 1, 0, 30),      # net_roll3o, default graph
     (75, 2, 8, 3, 1, 5, 30),      # net_roll3o, custom graph (3 draws per step)
     (30, 8, 4, 1, 0, 0, 30),      # im_roll3 / net_roll (2 roles: nch barriers)
-    (61, 4, 4, 1, 1, 29, 30),     # im_roll3o, a reset early in the launch
+    (61, 2, 8, 1, 1, 29, 30),     # im_roll3o, a reset early in the launch
+    (61, 4, 4, 1, 1, 29, 30),     # im_roll3o (CH, RD) = (4, 4) A/B build
     (40, 2, 8, 1, 1, 0, 4),       # resets in most chunks
     (9, 8, 4, 1, 0, 3, 30),       # a partial last chunk
     (2, 2, 8, 3, 1, 30, 30),      # the first step is a reset
