@@ -71,6 +71,8 @@ def parse():
                     help="step mode: skip the K-step rollout region reported under 'rollout'")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--pool", type=int, default=16, help="distinct action batches cycled")
+    ap.add_argument("--demand-stream", default="numpy", choices=["numpy", "philox"],
+                    help="numpy: the reference's PCG64 stream (parity, default); philox: the opt-in fast stream")
     return ap.parse_args()
 
 
@@ -268,7 +270,9 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     ep = stats.allreduce()                                  # RCCL all-reduce of the timed batch's statistics
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / calls
     total_steps = calls * steps_per_call
-    B = wl["B_io"] + (wl["B_state_rollout"] / K if K else wl["B_state"])
+    # the fast stream reads an 8-B key instead of the 32-B PCG64 state and writes no state back
+    dB = -40 if env.demand_stream == "philox" else 0
+    B = wl["B_io"] + ((wl["B_state_rollout"] + dB) / K if K else wl["B_state"] + dB)
     achieved = B * N * steps_per_call / (kern_ms * 1e-3) / 1e9
     achieved_wall = B * N * total_steps / el / 1e9
     return dict(el=el, calls=calls, warm=warm, steps_per_call=steps_per_call, total_steps=total_steps,
@@ -338,12 +342,13 @@ def main():
     n = args.n_envs or wl["n"]
     if args.strong:
         n = (n + world - 1) // world                      # this rank's share of the global batch
-    env = getattr(invsim, wl["cls"])(n, device=dev, global_offset=rank * n, copy=False)
+    env = getattr(invsim, wl["cls"])(n, device=dev, global_offset=rank * n, copy=False,
+                                     demand_stream=args.demand_stream)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
     env.reset(seed=0)
     r = run_region(args, env, wl, args.mode, args.steps, args.warmup, world, dev, gen, dist)
-    full = n == wl["n"] and not args.strong
+    full = n == wl["n"] and not args.strong and args.demand_stream == "numpy"   # the PMC files are of that run
     traffic, traffic_src = _pmc(args.workload, args.mode, full)
     N = r["N"]
     out = {
@@ -363,7 +368,7 @@ def main():
         "config": {"workload": wl["desc"], "envs_per_gpu": N, "global_envs": N * world,
                    "mode": args.mode + (f" K={r['K']}" if r["K"] else ""), "autoreset": "next_step",
                    "parallelism": f"dp{world} (env sharding, no data-path collective)",
-                   "backend": (backend if world > 1 else None)},
+                   "backend": (backend if world > 1 else None), "demand_stream": args.demand_stream},
         "roofline": _roofline(r, traffic, traffic_src),
         "episode_stats": dict(r["ep"], source="timed batch: HIP episode fold of the timed steps' rewards and "
                                               "done flags, one all-reduce after the region"),

@@ -250,6 +250,24 @@ int invsim_episode_fold(const double *reward, const uint8_t *terminated, const u
  * distributions.c, SURVEY App. B.) */
 int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear);
 
+/* Demand stream of a handle.  INVSIM_DEMAND_NUMPY (default): numpy's PCG64
+ * Generator stream and samplers, bit-exact with the reference on the same
+ * seeds (newsvendor.py:146, inventory_management.py:172,
+ * network_management.py:540).  INVSIM_DEMAND_PHILOX: an opt-in, NON-parity
+ * fast stream: rocRAND's Philox4x32-10 used counter-based,
+ * key = the env's seeded PCG64 increment (high word), counter = (block, draw
+ * stream, handle launch step); the same PTRS / multiplication / binomial /
+ * integers / geometric transforms.  No per-env generator state is read or
+ * written per step.  Every step / rollout step (and a Newsvendor reset)
+ * advances the handle's launch-step counter, which get_state / set_state carry
+ * ("philox_step"; the first fast-stream call after set_state reads it back,
+ * synchronously).  Switching streams synchronises the device once; the PCG64
+ * states are untouched by fast-stream steps. */
+#define INVSIM_DEMAND_NUMPY 0
+#define INVSIM_DEMAND_PHILOX 1
+int invsim_set_demand_stream(invsim_handle *h, int32_t mode);
+int invsim_demand_stream(const invsim_handle *h, int32_t *mode);
+
 /* Which kernel a handle runs: 0 = the generic kernel of its family, 1 / 2 =
  * NetInvMgmt specialised at compile time for the reference's default /
  * custom supply network (chosen at create when the graph equals one of them). */

@@ -35,6 +35,7 @@ int net_spec_match(const invsim_netinvmgmt_spec &h);   // netspec.hip
 #ifdef INVSIM_PTRS_STATS
 hipError_t ptrs_stats_nv(unsigned long long *out, bool clear);
 hipError_t ptrs_stats_im(unsigned long long *out, bool clear);
+hipError_t ptrs_stats_im_ph(unsigned long long *out, bool clear);
 hipError_t ptrs_stats_netspec(unsigned long long *out, bool clear);
 hipError_t ptrs_stats_net(unsigned long long *out, bool clear);
 #endif
@@ -64,6 +65,13 @@ struct invsim_handle {
     int32_t t_cur = 0;
     int32_t horizon = 0;
     bool past_ok = false;     // Newsvendor keeps stepping past step_limit with autoreset off
+    // demand stream (invsim_set_demand_stream): numpy PCG64 (parity) or the fast
+    // counter-based Philox stream, whose launch-step counter lives here and in
+    // the state blob ("philox_step")
+    int32_t demand_stream = INVSIM_DEMAND_NUMPY;
+    uint64_t ph_step = 0;
+    int64_t o_phstep = 0;
+    bool ph_from_blob = false;  // set_state loaded the blob: its philox_step is the counter
     std::string err;
 };
 
@@ -155,6 +163,7 @@ int common_fields(invsim_handle *h, Layout &lay, int64_t &o_rng, int64_t &o_peri
     o_rng = lay.add("rng", 8, 4, h->Npad);   // rows: state_hi, state_lo, inc_hi, inc_lo
     o_period = lay.add("period", 4, 1, h->Npad);
     o_status = lay.add("status", 4, 1, 1);
+    h->o_phstep = lay.add("philox_step", 8, 1, 1);
     return 0;
 }
 
@@ -652,6 +661,21 @@ static void sync_common(invsim_handle *h) {
     h->net.cm = h->cm;
 }
 
+// the fast stream's counter into the kernel parameters (after set_state: from
+// the blob first, which is the one synchronising read of that stream)
+static int ph_counter_sync(invsim_handle *h, hipStream_t s) {
+    if (h->ph_from_blob) {
+        hipError_t e = hipMemcpyAsync(&h->ph_step, h->arena + h->o_phstep, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(h, e, "philox_step read");
+        h->ph_from_blob = false;
+    }
+    h->cm.ph_step = h->ph_step;
+    sync_common(h);
+    return INVSIM_OK;
+}
+
+
 int invsim_set_autoreset(invsim_handle *h, int32_t mode) {
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (!valid_autoreset(mode)) return fail(h, INVSIM_EINVAL, "bad autoreset mode");
@@ -739,10 +763,15 @@ int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream)
         int rc = materialize_period(h, s);
         if (rc != INVSIM_OK) return rc;
     }
-    if (h->family == INVSIM_NEWSVENDOR) {   // its reset draws from cm.rng
+    if (h->family == INVSIM_NEWSVENDOR) {   // its reset draws from cm.rng (or the fast stream)
         int rc = commit_rng(h, s);
         if (rc != INVSIM_OK) return rc;
         h->la_valid = false;
+        if (h->demand_stream == INVSIM_DEMAND_PHILOX) {
+            rc = ph_counter_sync(h, s);
+            if (rc != INVSIM_OK) return rc;
+            h->ph_step += 1;                  // the reset's uniforms own a counter value
+        }
     }
     hipError_t e = hipSuccess;
     switch (h->family) {
@@ -776,6 +805,10 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
             t = next_period(t, h->horizon, h->cm.autoreset, h->past_ok);
         }
     }
+    if (h->demand_stream == INVSIM_DEMAND_PHILOX) {
+        int rc = ph_counter_sync(h, s);
+        if (rc != INVSIM_OK) return rc;
+    }
     hipError_t e = hipSuccess;
     switch (h->family) {
         case INVSIM_NEWSVENDOR: {
@@ -801,6 +834,7 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         h->la_valid = false;
         return hip_fail(h, e, "step launch");
     }
+    if (h->demand_stream == INVSIM_DEMAND_PHILOX) h->ph_step += (uint64_t)K;   // one counter value per launch step
     if (h->t_known) {
         for (int k = 0; k < K; k++) h->t_cur = next_period(h->t_cur, h->horizon, h->cm.autoreset, h->past_ok);
     } else if (h->cm.autoreset == AR_DISABLED && !h->past_ok) {
@@ -926,8 +960,8 @@ int invsim_episode_fold(const double *reward, const uint8_t *terminated, const u
 int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear) {
     if (!out) return fail(nullptr, INVSIM_EINVAL, "null argument");
 #ifdef INVSIM_PTRS_STATS
-    hipError_t (*tus[4])(unsigned long long *, bool) = {ptrs_stats_nv, ptrs_stats_im, ptrs_stats_netspec,
-                                                        ptrs_stats_net};
+    hipError_t (*tus[5])(unsigned long long *, bool) = {ptrs_stats_nv, ptrs_stats_im, ptrs_stats_im_ph,
+                                                        ptrs_stats_netspec, ptrs_stats_net};
     out[0] = out[1] = out[3] = 0;
     out[2] = 0x7ff0000000000000ull;
     for (auto f : tus) {
@@ -945,6 +979,30 @@ int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear) {
     (void)clear;
     return fail(nullptr, INVSIM_EINVAL, "not a PTRS-statistics build (make -C csrc ptrs_stats)");
 #endif
+}
+
+int invsim_set_demand_stream(invsim_handle *h, int32_t mode) {
+    TraceRange tr_("invsim_set_demand_stream");
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (mode != INVSIM_DEMAND_NUMPY && mode != INVSIM_DEMAND_PHILOX)
+        return fail(h, INVSIM_EINVAL, "demand stream must be INVSIM_DEMAND_NUMPY or INVSIM_DEMAND_PHILOX");
+    if (mode == h->demand_stream) return INVSIM_OK;
+    DeviceGuard g(h->device);
+    int rc = commit_rng(h, nullptr);   // the parity stream's lookahead cache ends (legacy stream)
+    if (rc != INVSIM_OK) return rc;
+    hipError_t e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) return hip_fail(h, e, "demand stream switch");
+    h->la_valid = false;
+    h->demand_stream = mode;
+    h->cm.philox = mode == INVSIM_DEMAND_PHILOX ? 1 : 0;
+    sync_common(h);
+    return INVSIM_OK;
+}
+
+int invsim_demand_stream(const invsim_handle *h, int32_t *mode) {
+    if (!h || !mode) return fail(nullptr, INVSIM_EINVAL, "null argument");
+    *mode = h->demand_stream;
+    return INVSIM_OK;
 }
 
 int invsim_kernel_variant(const invsim_handle *h, int32_t *variant) {
@@ -984,7 +1042,7 @@ int invsim_state_field(const invsim_handle *h, int32_t idx, char name[32], int64
     if (elem_bytes) *elem_bytes = f.elem;
     if (rows) *rows = f.rows;
     // > 0: [rows][row_stride]; < 0: record layout [-row_stride][rows]; 0: other layout
-    if (row_stride) *row_stride = (f.name == "status") ? 1 : f.kind == 1 ? -h->Npad : f.kind == 2 ? 0 : h->Npad;
+    if (row_stride) *row_stride = (f.name == "status" || f.name == "philox_step") ? 1 : f.kind == 1 ? -h->Npad : f.kind == 2 ? 0 : h->Npad;
     return INVSIM_OK;
 }
 
@@ -995,6 +1053,12 @@ int invsim_get_state(invsim_handle *h, void *dst, void *stream) {
     int rc = materialize_period(h, (hipStream_t)stream);  // the blob carries per-env periods
     if (rc == INVSIM_OK) rc = commit_rng(h, (hipStream_t)stream);   // and the committed PCG64 states
     if (rc != INVSIM_OK) return rc;
+    if (!h->ph_from_blob) {                                // and the fast stream's counter
+        hipError_t e0 = hipMemcpyAsync(h->arena + h->o_phstep, &h->ph_step, sizeof(uint64_t),
+                                       hipMemcpyHostToDevice, (hipStream_t)stream);
+        if (e0 == hipSuccess) e0 = hipStreamSynchronize((hipStream_t)stream);   // the host word may change next
+        if (e0 != hipSuccess) return hip_fail(h, e0, "philox_step write");
+    }
     hipError_t e = hipMemcpyAsync(dst, h->arena, (size_t)h->arena_bytes, hipMemcpyDeviceToDevice,
                                   (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "get_state");
@@ -1009,6 +1073,7 @@ int invsim_set_state(invsim_handle *h, const void *src, void *stream) {
     if (e != hipSuccess) return hip_fail(h, e, "set_state");
     h->t_known = false;  // periods now come from the blob
     h->la_valid = false;
+    h->ph_from_blob = true;   // and the fast stream's counter (read when next needed)
     return INVSIM_OK;
 }
 

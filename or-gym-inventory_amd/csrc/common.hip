@@ -58,17 +58,30 @@ episode_fold_kernel(const double *rew, const uint8_t *term, const uint8_t *trunc
     double s = 0.0, s2 = 0.0, c = 0.0, all = 0.0;
     if (e < N) {
         double r = ret[e];
-        for (int k = 0; k < K; ++k) {
-            const int64_t i = (int64_t)k * N + e;
-            const double x = rew[i];
-            r += x;
-            all += x;
-            const bool d = (term && term[i]) || (trunc && trunc[i]);
-            if (d) {
-                s += r;
-                s2 += r * r;
-                c += 1.0;
-                r = 0.0;
+        // rows in blocks of FB with every load of a block issued before the first
+        // add: one memory latency per block instead of one per row
+        constexpr int FB = 16;
+        for (int k0 = 0; k0 < K; k0 += FB) {
+            double x[FB];
+            uint8_t d[FB];
+#pragma unroll
+            for (int u = 0; u < FB; ++u) {
+                const int64_t i = (int64_t)min(k0 + u, K - 1) * N + e;
+                x[u] = rew[i];
+                d[u] = (uint8_t)((term ? term[i] : 0) | (trunc ? trunc[i] : 0));
+            }
+#pragma unroll
+            for (int u = 0; u < FB; ++u) {
+                if (k0 + u < K) {
+                    r += x[u];
+                    all += x[u];
+                    if (d[u]) {
+                        s += r;
+                        s2 += r * r;
+                        c += 1.0;
+                        r = 0.0;
+                    }
+                }
             }
         }
         ret[e] = r;

@@ -13,6 +13,7 @@
 // Poisson acceptance tests must see the same roundings.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <rocrand/rocrand_philox4x32_10.h>
 #include <stdint.h>
 
 namespace invsim {
@@ -35,6 +36,57 @@ struct Pcg {
         uint64_t x = hi ^ lo;
         unsigned rot = (unsigned)(hi >> 58);
         return (x >> rot) | (x << ((64u - rot) & 63u));
+    }
+    __device__ __forceinline__ double next_double() {
+        return (double)(next64() >> 11) * (1.0 / 9007199254740992.0);
+    }
+    // counter positioning of the fast stream (PhiloxGen): a sequential stream has none
+    static constexpr bool kCounter = false;
+    __device__ __forceinline__ void set_step(uint64_t) {}
+    __device__ __forceinline__ void sub(uint32_t) {}
+};
+
+// ---------------------------------------------------------------- fast stream
+// Opt-in, NON-parity demand stream (invsim_set_demand_stream):
+// rocRAND's Philox4x32-10 block function used counter-based.  An env's key is
+// its seeded PCG64 increment (high word: 64 bits of SeedSequence output), and
+// the counter of draw block j of stream r (0 = demand / market r, RESET = the
+// Newsvendor reset's uniforms) in launch step s of the handle is (j, r, s_lo,
+// s_hi).  So a draw depends on (seed, step, r) only: no generator state is read
+// or written per step, and no draw waits for the previous one.  The samplers
+// (PTRS / multiplication / numpy_dists) are the parity ones, fed with 53-bit
+// uniforms from the 128-bit blocks (two per block).
+struct PhiloxBlock : rocrand_device::philox4x32_10_engine {
+    __device__ __forceinline__ uint4 block(uint4 c, uint2 k) { return this->ten_rounds(c, k); }
+};
+
+struct PhiloxGen {
+    static constexpr uint32_t RESET = 0xffffffffu;
+    static constexpr bool kCounter = true;
+    uint2 key;
+    uint32_t s0 = 0, s1 = 0, r = 0, j = 0;
+    uint64_t hold = 0;
+    bool have = false;
+    __device__ __forceinline__ void set_step(uint64_t s) {
+        s0 = (uint32_t)s;
+        s1 = (uint32_t)(s >> 32);
+    }
+    __device__ __forceinline__ void sub(uint32_t rr) {
+        r = rr;
+        j = 0;
+        have = false;
+    }
+    __device__ __forceinline__ uint64_t next64() {
+        if (have) {
+            have = false;
+            return hold;
+        }
+        PhiloxBlock b;
+        const uint4 x = b.block(make_uint4(j, r, s0, s1), key);
+        j++;
+        hold = ((uint64_t)x.w << 32) | x.z;
+        have = true;
+        return ((uint64_t)x.y << 32) | x.x;
     }
     __device__ __forceinline__ double next_double() {
         return (double)(next64() >> 11) * (1.0 / 9007199254740992.0);
@@ -221,7 +273,8 @@ __device__ __forceinline__ bool ptrs_log_accept(const PtrsConst &c, double V, do
 }
 
 // numpy random_poisson_ptrs (distributions.c), constants precomputed
-__device__ inline int64_t np_poisson_ptrs(Pcg &g, const PtrsConst &c, const double *rhs = nullptr) {
+template <class G>
+__device__ inline int64_t np_poisson_ptrs(G &g, const PtrsConst &c, const double *rhs = nullptr) {
     for (;;) {
         double U = g.next_double() - 0.5;
         double V = g.next_double();
@@ -234,7 +287,8 @@ __device__ inline int64_t np_poisson_ptrs(Pcg &g, const PtrsConst &c, const doub
 }
 
 // numpy random_poisson_mult (0 < lam < 10), enlam = exp(-lam)
-__device__ inline int64_t np_poisson_mult(Pcg &g, double enlam) {
+template <class G>
+__device__ inline int64_t np_poisson_mult(G &g, double enlam) {
     int64_t X = 0;
     double prod = 1.0;
     for (;;) {
@@ -247,7 +301,8 @@ __device__ inline int64_t np_poisson_mult(Pcg &g, double enlam) {
 }
 
 // numpy random_poisson with host-precomputed constants (fixed lam)
-__device__ __forceinline__ int64_t np_poisson(Pcg &g, const PtrsConst &c, const double *rhs = nullptr) {
+template <class G>
+__device__ __forceinline__ int64_t np_poisson(G &g, const PtrsConst &c, const double *rhs = nullptr) {
     if (c.lam >= 10) return np_poisson_ptrs(g, c, rhs);
     if (c.lam == 0) return 0;
     return np_poisson_mult(g, c.enlam);
@@ -255,7 +310,8 @@ __device__ __forceinline__ int64_t np_poisson(Pcg &g, const PtrsConst &c, const 
 
 // numpy random_poisson_ptrs for a per-env lam with a (lam-independent) table of
 // loggam(k + 1), k < lgn, computed on the host with numpy's own formula
-__device__ inline int64_t np_poisson_ptrs_lg(Pcg &g, const PtrsConst &c, const double *lgtab, int lgn) {
+template <class G>
+__device__ inline int64_t np_poisson_ptrs_lg(G &g, const PtrsConst &c, const double *lgtab, int lgn) {
     for (;;) {
         double U = g.next_double() - 0.5;
         double V = g.next_double();
@@ -270,7 +326,8 @@ __device__ inline int64_t np_poisson_ptrs_lg(Pcg &g, const PtrsConst &c, const d
 }
 
 // numpy random_poisson for a per-env lam: only the branch's constants are computed
-__device__ inline int64_t np_poisson_dyn(Pcg &g, double lam, const double *lgtab, int lgn) {
+template <class G>
+__device__ inline int64_t np_poisson_dyn(G &g, double lam, const double *lgtab, int lgn) {
     if (lam >= 10) {
         PtrsConst c;
         c.lam = lam;
@@ -291,7 +348,8 @@ __device__ inline int64_t np_poisson_dyn(Pcg &g, double lam, const double *lgtab
 }
 
 // numpy random_poisson for a per-env lam: only the branch's constants are computed
-__device__ inline int64_t np_poisson_dyn(Pcg &g, double lam) {
+template <class G>
+__device__ inline int64_t np_poisson_dyn(G &g, double lam) {
     if (lam >= 10) {
         PtrsConst c;
         c.lam = lam;
@@ -358,6 +416,14 @@ struct RngSoA {
         inc_hi[e] = g.inc_hi;
         inc_lo[e] = g.inc_lo;
     }
+    // a step kernel's generator: the PCG64 stream (32 B in, 16 B out per env) or
+    // the fast stream's key (8 B in, nothing out)
+    __device__ __forceinline__ void load(int64_t e, Pcg &g) const { g = load(e); }
+    __device__ __forceinline__ void load(int64_t e, PhiloxGen &g) const {
+        const uint64_t k = inc_hi[e];
+        g.key = make_uint2((uint32_t)k, (uint32_t)(k >> 32));
+    }
+    __device__ __forceinline__ void store_state(int64_t, const PhiloxGen &) const {}
 };
 
 }  // namespace invsim

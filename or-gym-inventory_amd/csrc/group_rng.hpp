@@ -165,8 +165,8 @@ struct PtrsJumpLane {
 
 // one PTRS candidate (numpy random_poisson_ptrs loop body) from two uniforms of
 // g; rhs(k, c) = -lam + k log lam - loggam(k + 1)
-template <class Rhs>
-__device__ __forceinline__ bool ptrs_candidate(Pcg &g, const PtrsConst &c, Rhs rhs, int64_t &k) {
+template <class G, class Rhs>
+__device__ __forceinline__ bool ptrs_candidate(G &g, const PtrsConst &c, Rhs rhs, int64_t &k) {
     const double U = g.next_double() - 0.5;
     const double V = g.next_double();
     const double us = 0.5 - fabs(U);

@@ -72,9 +72,9 @@ struct ImPending {
     int t;
 };
 
-template <int M1, bool BACKLOG>
+template <int M1, bool BACKLOG, class G = Pcg>
 struct ImState {
-    Pcg g;
+    G g;
     uint64_t u32;        // PCG64 32-bit buffer (dist 3 only)
     int64_t I[M1];
     int64_t B[M1 + 1];
@@ -82,8 +82,8 @@ struct ImState {
 
 // reset (:197-220): I = I0, B = 0; obs row = [I0, 0...] (lane j of the group
 // writes every 4th element)
-template <int M1, bool BACKLOG>
-__device__ __forceinline__ void im_reset_regs(const ImParams &P, ImState<M1, BACKLOG> &s,
+template <int M1, bool BACKLOG, class G = Pcg>
+__device__ __forceinline__ void im_reset_regs(const ImParams &P, ImState<M1, BACKLOG, G> &s,
                                               int64_t *orow, int j) {
 #pragma unroll
     for (int i = 0; i < M1; i++) s.I[i] = P.I0[i];
@@ -96,9 +96,9 @@ __device__ __forceinline__ void im_reset_regs(const ImParams &P, ImState<M1, BAC
 }
 
 // One step (:224-352) at period t < periods.  Returns truncated.
-template <int M1, bool BACKLOG, bool NPD>
+template <int M1, bool BACKLOG, bool NPD, class G = Pcg>
 __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool valid, int j, int t,
-                                             ImState<M1, BACKLOG> &s,
+                                             ImState<M1, BACKLOG, G> &s,
                                              const int64_t *__restrict__ arow, int64_t *orow,
                                              const double *rhs, TableStage *ts, double apow, int64_t udem,
                                              double &reward, int64_t &dem_out, double *met, int64_t *irec,
@@ -160,6 +160,8 @@ __device__ __forceinline__ bool im_step_regs(const ImParams &P, int64_t e, bool 
 #ifdef INVSIM_ABL_NO_POISSON  // profiling ablation build only (wrong results)
     int64_t d = 20 + (int64_t)(s.g.lo & 3);
 #else
+    s.g.sub(0);
+    if constexpr (G::kCounter) s.u32 = 0;    // fast stream: no 32-bit half carried between steps
     int64_t d = NPD ? np_demand(s.g, s.u32, P.nd) : (P.dist == 5) ? udem : env_poisson(s.g, P.pc, rhs);
 #endif
     if (d < 0) d = 0;
@@ -312,8 +314,8 @@ __device__ __forceinline__ void im_flush_pending(const ImParams &P, const ImPend
 // up to (L_i + 1) * mu * sf over the inventory position on hand + requested
 // orders of the last L_i periods (action_log[max(0, t - L_i) : t, i]), in
 // float64, clipped to [0, c_i], truncated to int64.
-template <int M1, bool BACKLOG>
-__device__ __forceinline__ void im_base_stock(const ImParams &P, const PolicyIO &pol, const ImState<M1, BACKLOG> &st,
+template <int M1, bool BACKLOG, class G = Pcg>
+__device__ __forceinline__ void im_base_stock(const ImParams &P, const PolicyIO &pol, const ImState<M1, BACKLOG, G> &st,
                                               int t, int64_t e, int64_t (&act)[M1]) {
     const int64_t S = P.cm.Npad;
     const int D = P.lt_max;
@@ -341,10 +343,10 @@ __device__ __forceinline__ void im_base_stock(const ImParams &P, const PolicyIO 
 
 // Step k of a launch for the wave's envs: step (or NEXT_STEP reset) into the
 // LDS obs tile, SAME_STEP final-obs/reset, then the tile's coalesced store.
-template <int M1, bool BACKLOG, bool STEP_ONLY, bool POL, bool NPD>
+template <int M1, bool BACKLOG, bool STEP_ONLY, bool POL, bool NPD, class G = Pcg>
 __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<int64_t, int64_t> &io, int k,
                                                int64_t e, int64_t e0, int lane, bool valid, int nvalid,
-                                               ImState<M1, BACKLOG> &st, int &t, bool &fault,
+                                               ImState<M1, BACKLOG, G> &st, int &t, bool &fault,
                                                int64_t *tile, int64_t *trow, const double *rhs,
                                                TableStage *ts, const double *pre_apow, const int64_t *pre_udem,
                                                const PolicyIO &pol, double *met) {
@@ -443,7 +445,7 @@ __device__ __forceinline__ void im_launch_step(const ImParams &P, const StepIO<i
     wave_lds_sync();
 }
 
-template <int M1, bool BACKLOG, bool TU, bool ONE, bool POL, bool NPD>
+template <int M1, bool BACKLOG, bool TU, bool ONE, bool POL, bool NPD, class G>
 __global__ void __launch_bounds__(WAVE)
 im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
@@ -503,9 +505,10 @@ im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     // state rows are Npad wide, so every lane loads unconditionally (straight-line
     // loads keep the compiler's vmcnt waits exact); lanes past N take the last
     // env's PCG64 stream (an all-zero stream would never leave the PTRS loop)
-    ImState<M1, BACKLOG> st;
-    st.g = P.cm.rng.load(valid ? e : N - 1);
-    st.u32 = NPD ? P.cm.u32buf[valid ? e : N - 1] : 0;
+    ImState<M1, BACKLOG, G> st;
+    P.cm.rng.load(valid ? e : N - 1, st.g);
+    st.g.set_step(P.cm.ph_step);
+    st.u32 = (NPD && !G::kCounter) ? P.cm.u32buf[valid ? e : N - 1] : 0;
 #pragma unroll
     for (int i = 0; i < M1; i++) st.I[i] = P.I[i * S + e];
 #pragma unroll
@@ -521,13 +524,15 @@ im_run_kernel(ImParams P, int t_u, StepIO<int64_t, int64_t> io, PolicyIO pol) {
                                                rhs_l, &ts, &apow0, &udem0, pol, met);
     } else {
         ts.flush(lane);
-        for (int k = 0; k < io.K; k++)
+        for (int k = 0; k < io.K; k++) {
+            st.g.set_step(P.cm.ph_step + (uint64_t)k);
             im_launch_step<M1, BACKLOG, false, POL, NPD>(P, io, k, e, e0, lane, valid, nvalid, st, t, fault, im_tile,
                                                     trow, rhs_l, nullptr, nullptr, nullptr, pol, met);
+        }
     }
     if (valid && leader) {
         P.cm.rng.store_state(e, st.g);
-        if (NPD) P.cm.u32buf[e] = st.u32;
+        if (NPD && !G::kCounter) P.cm.u32buf[e] = st.u32;
 #pragma unroll
         for (int i = 0; i < M1; i++) st_store(P.I + i * S + e, st.I[i]);
         if (BACKLOG) {
@@ -1514,6 +1519,45 @@ inline bool im_ahead_enabled() {
         default: return hipErrorInvalidValue;                          \
     }
 
+#ifdef INVSIM_IM_FAST_TU
+// invmgmt_ph.hip: this file compiled a second time for the fast-stream run
+// kernels (a TU of their own, so the two instantiation sets compile in parallel)
+hipError_t im_run_launch_ph(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
+                            const StepIO<int64_t, int64_t> &io, hipStream_t s) {
+    if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
+    const size_t lds = (size_t)EPW * M1 * (p.lt_max + 1) * sizeof(int64_t) + RHS_LDS_MAX * sizeof(double);
+    const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
+    PolicyIO none{};
+    const PolicyIO &pv = pol ? *pol : none;
+    const bool npd = p.dist >= 2 && p.dist <= 4;
+#define K_(M, B, TU, ONE, POL)                                                                          \
+    do {                                                                                                \
+        if (npd)                                                                                        \
+            hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL, true, PhiloxGen>), grid, block, lds, s, p, t_u, io, pv);  \
+        else                                                                                            \
+            hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL, false, PhiloxGen>), grid, block, lds, s, p, t_u, io, pv); \
+    } while (0)
+#define L_(M, B)                                             \
+    do {                                                     \
+        if (pol) {                                           \
+            if (t_u >= 0) K_(M, B, true, false, true);       \
+            else K_(M, B, false, false, true);               \
+        } else if (io.K == 1) {                              \
+            if (t_u >= 0) K_(M, B, true, true, false);       \
+            else K_(M, B, false, true, false);               \
+        } else {                                             \
+            if (t_u >= 0) K_(M, B, true, false, false);      \
+            else K_(M, B, false, false, false);              \
+        }                                                    \
+    } while (0)
+    IM_DISPATCH(M1, backlog, L_)
+#undef L_
+#undef K_
+    return hipGetLastError();
+}
+
+INVSIM_PTRS_STATS_TU(im_ph)
+#else
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
                          const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
@@ -1522,6 +1566,15 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
     const bool npd = p.dist >= 2 && p.dist <= 4;
+    const bool ph = p.cm.philox != 0;       // fast stream: the run kernels only (no lookahead, no demand waves)
+    if (ph) {
+        if (ahead) {                        // the parity stream's lookahead cache ends here
+            const hipError_t ce = im_commit_launch(p, slot, s);
+            ahead = false;
+            if (ce != hipSuccess) return ce;
+        }
+        return im_run_launch_ph(p, M1, backlog, t_u, pol, io, s);
+    }
     if (!pol && io.K == 1 && t_u >= 0 && t_u < p.periods && io.obs &&
         !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.periods) && im_split_enabled()) {
         const size_t lds2 = lds + WAVE * sizeof(int64_t);
@@ -1589,9 +1642,9 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
 #define K_(M, B, TU, ONE, POL)                                                                         \
     do {                                                                                                \
         if (npd)                                                                                        \
-            hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL, true>), grid, block, lds, s, p, t_u, io, pv);  \
+            hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL, true, Pcg>), grid, block, lds, s, p, t_u, io, pv);  \
         else                                                                                            \
-            hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL, false>), grid, block, lds, s, p, t_u, io, pv); \
+            hipLaunchKernelGGL((im_run_kernel<M, B, TU, ONE, POL, false, Pcg>), grid, block, lds, s, p, t_u, io, pv); \
     } while (0)
 #define L_(M, B)                                             \
     do {                                                     \
@@ -1629,10 +1682,11 @@ hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_
 }
 
 INVSIM_PTRS_STATS_TU(im)
+#endif  // INVSIM_IM_FAST_TU
 
 }  // namespace invsim
 
-#ifdef INVSIM_TIMING
+#if defined(INVSIM_TIMING) && !defined(INVSIM_IM_FAST_TU)
 extern "C" int invsim_debug_timing(void *dst, int64_t bytes) {
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_tbuf), (size_t)bytes, 0, hipMemcpyDeviceToHost);
 }

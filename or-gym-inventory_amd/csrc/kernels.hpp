@@ -55,6 +55,8 @@ struct Common {
     uint32_t *status;      // sticky error word (DISABLED-mode overrun)
     uint64_t *u32buf;      // [Npad] PCG64 32-bit output buffer (has << 32 | value), or null
     void *info_rec;        // optional per-step info record (invsim_set_info_record), last step of a launch
+    int32_t philox;        // demand stream: 0 numpy PCG64 (parity), 1 fast Philox (PhiloxGen)
+    uint64_t ph_step;      // fast stream: the handle's launch-step counter at this launch's first step
 };
 
 // ---------------------------------------------------------------- Newsvendor
@@ -184,15 +186,18 @@ constexpr int RHS_LDS_MAX = 512;  // PTRS RHS table entries per Poisson rate (st
 constexpr int LPE = 1;
 constexpr int EPW = WAVE / LPE;   // envs per wave
 
-__device__ __forceinline__ int64_t env_poisson(Pcg &g, const PtrsConst &c, const double *rhs) {
-    if (LPE == 1) return np_poisson(g, c, rhs);
-    return np_poisson_grp(g, c, rhs);
+template <class G>
+__device__ __forceinline__ int64_t env_poisson(G &g, const PtrsConst &c, const double *rhs) {
+    if constexpr (LPE == 1) return np_poisson(g, c, rhs);
+    else return np_poisson_grp(g, c, rhs);
 }
-__device__ __forceinline__ int64_t env_poisson_dyn(Pcg &g, double lam) {
-    if (LPE == 1) return np_poisson_dyn(g, lam);
-    return np_poisson_dyn_grp(g, lam);
+template <class G>
+__device__ __forceinline__ int64_t env_poisson_dyn(G &g, double lam) {
+    if constexpr (LPE == 1) return np_poisson_dyn(g, lam);
+    else return np_poisson_dyn_grp(g, lam);
 }
-__device__ __forceinline__ int64_t env_poisson_dyn(Pcg &g, double lam, const double *lgtab, int lgn) {
+template <class G>
+__device__ __forceinline__ int64_t env_poisson_dyn(G &g, double lam, const double *lgtab, int lgn) {
     return np_poisson_dyn(g, lam, lgtab, lgn);
 }
 
@@ -301,7 +306,8 @@ __device__ __forceinline__ void roll_wg_sync() {
 // whole multiplication-method draw (0 < lam < 10), or 0 (lam == 0) -- the
 // branches of np_poisson, so the attempts up to the first `true` consume the
 // stream exactly as one np_poisson call.
-__device__ __forceinline__ bool np_poisson_try(Pcg &g, const PtrsConst &c, const double *rhs, int64_t &k) {
+template <class G>
+__device__ __forceinline__ bool np_poisson_try(G &g, const PtrsConst &c, const double *rhs, int64_t &k) {
     if (c.lam >= 10) return ptrs_candidate(g, c, [&](int64_t kk, const PtrsConst &cc) { return ptrs_rhs(cc, rhs, kk); }, k);
     k = (c.lam == 0) ? 0 : np_poisson_mult(g, c.enlam);
     return true;
@@ -367,6 +373,9 @@ hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_
 // slot (updated) does now
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
                          const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s);
+// the fast-stream (cm.philox) run kernels, invmgmt_ph.hip
+hipError_t im_run_launch_ph(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
+                            const StepIO<int64_t, int64_t> &io, hipStream_t s);
 // cm.rng <- the committed generator state held by the lookahead cache (whose
 // current slot is `slot`); needed before anything reads cm.rng while it is valid
 hipError_t im_commit_launch(const ImParams &p, int slot, hipStream_t s);

@@ -57,7 +57,8 @@ __device__ __forceinline__ void net_reset_lds(const NetParams &P, NetScratch &s,
 // All LPE lanes of the env run it (redundant node/link arithmetic in private
 // LDS scratch, lane-group Poisson draws); lane j == 0 writes state and the
 // U/X part of the obs row, lane j writes the order windows of links k = j mod LPE.
-__device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, Pcg &g, NetScratch &s,
+template <class RG>
+__device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, RG &g, NetScratch &s,
                              const float *__restrict__ arow, float *orow, double &reward, int64_t *dem,
                              double *irec) {
     const int64_t S = P.cm.Npad;
@@ -72,6 +73,7 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, Pcg &
             if (!(dd > 0)) dd = 0.0;
         } else {
             const PtrsConst &pc = P.rl_pc[r];
+            g.sub((uint32_t)r);                                // fast stream: market r's counter block
             const int64_t pd = env_poisson(g, pc, P.rhs ? P.rhs + pc.toff : nullptr);
             dd = (double)(pd > 0 ? pd : 0);
         }
@@ -204,7 +206,7 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, Pcg &
 // (ConstantOrderAgent, benchmark_NetInvMgmtBacklogEnv.py:119-135) on any graph:
 // every output optional, evaluate_agent metrics (as net_spec_kernel) summed
 // into pol.metrics in place.
-template <bool TU, bool POL>
+template <bool TU, bool POL, class RG>
 __global__ void __launch_bounds__(WAVE)
 net_run_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) double net_lds[];
@@ -223,10 +225,10 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     float *tile = reinterpret_cast<float *>(net_lds + (int64_t)rows * WAVE);
     float *trow = tile + (int64_t)(lane / LPE) * O;
 
-    Pcg g;
+    RG g;
     int t = t_u;
     if (valid) {
-        g = P.cm.rng.load(e);
+        P.cm.rng.load(e, g);
         for (int j = 0; j < P.J; j++) LV(s.X, j) = P.X[j * S + e];
         for (int r = 0; r < P.RL; r++) LV(s.U, r) = P.U[r * S + e];
         for (int k = 0; k < P.E; k++) LV(s.Y, k) = P.Y[k * S + e];
@@ -236,6 +238,7 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     for (int k = 0; k < io.K; k++) {
         const int64_t oi = (int64_t)k * N + e;
         bool tr = false;
+        g.set_step(P.cm.ph_step + (uint64_t)k);
         if (valid) {
             if (t >= P.T) {
                 if (P.cm.autoreset == AR_NEXT_STEP) {
@@ -344,13 +347,19 @@ hipError_t net_run_launch(const NetParams &p, int t_u, const PolicyIO *pol, cons
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
     if (pol && pol->kind != POL_CONSTANT) return hipErrorInvalidValue;
+#define K_(TU, POL)                                                                                    \
+    do {                                                                                               \
+        if (p.cm.philox) hipLaunchKernelGGL((net_run_kernel<TU, POL, PhiloxGen>), grid, block, lds, s, p, t_u, io, pv); \
+        else hipLaunchKernelGGL((net_run_kernel<TU, POL, Pcg>), grid, block, lds, s, p, t_u, io, pv);         \
+    } while (0)
     if (t_u >= 0) {
-        if (pol) hipLaunchKernelGGL((net_run_kernel<true, true>), grid, block, lds, s, p, t_u, io, pv);
-        else hipLaunchKernelGGL((net_run_kernel<true, false>), grid, block, lds, s, p, t_u, io, pv);
+        if (pol) K_(true, true);
+        else K_(true, false);
     } else {
-        if (pol) hipLaunchKernelGGL((net_run_kernel<false, true>), grid, block, lds, s, p, t_u, io, pv);
-        else hipLaunchKernelGGL((net_run_kernel<false, false>), grid, block, lds, s, p, t_u, io, pv);
+        if (pol) K_(false, true);
+        else K_(false, false);
     }
+#undef K_
     return hipGetLastError();
 }
 

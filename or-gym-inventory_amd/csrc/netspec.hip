@@ -23,9 +23,9 @@ namespace {
 
 __device__ __forceinline__ double max0(double x) { return (x > 0) ? x : 0.0; }
 
-template <class G>
+template <class G, class RG = Pcg>
 struct NetSt {
-    Pcg g;
+    RG g;
     double X[G::J];
     double U[G::RL];
     double Y[G::E];
@@ -38,8 +38,8 @@ __device__ __forceinline__ int ring_row(int k, int t, int a) {
     return G::ring_off[k] + (int)((uint32_t)(t - a) % (uint32_t)G::L[k]);
 }
 
-template <class G>
-__device__ __forceinline__ void spec_reset(NetSt<G> &s, float *orow) {
+template <class G, class RG = Pcg>
+__device__ __forceinline__ void spec_reset(NetSt<G, RG> &s, float *orow) {
 #pragma unroll
     for (int j = 0; j < G::J; j++) s.X[j] = G::I0[j];
 #pragma unroll
@@ -58,11 +58,12 @@ __device__ __forceinline__ void spec_reset(NetSt<G> &s, float *orow) {
 
 // market demand draws of one step, retail-link order: max(0, int(round(poisson(lam))))
 // (:536-541)
-template <class G>
-__device__ __forceinline__ void spec_demand(Pcg &g, const PtrsConst (&pc)[G::RL], const double *rhs_l,
+template <class G, class RG>
+__device__ __forceinline__ void spec_demand(RG &g, const PtrsConst (&pc)[G::RL], const double *rhs_l,
                                             double (&Dd)[G::RL]) {
 #pragma unroll
     for (int r = 0; r < G::RL; r++) {
+        g.sub((uint32_t)r);                                    // fast stream: market r's counter block
         const int64_t pd = np_poisson(g, pc[r], rhs_l + r * RHS_LDS_MAX);
         Dd[r] = (double)(pd > 0 ? pd : 0);
     }
@@ -103,8 +104,8 @@ __device__ __forceinline__ void net_demand_loop(Pcg &g, const PtrsConst (&pc)[G:
 //
 // spec_core: the step without the observation, given each link's age-L window
 // entry wa[k] = R[t - L_k] (the arrival; unused for L == 0).
-template <class G>
-__device__ __forceinline__ double spec_core(const NetParams &P, double apow, NetSt<G> &s,
+template <class G, class RG = Pcg>
+__device__ __forceinline__ double spec_core(const NetParams &P, double apow, NetSt<G, RG> &s,
                                             const float (&act)[G::E], const double (&Dd)[G::RL],
                                             const double (&wa)[G::E], double (&Rn)[G::E], double *met,
                                             double *irec) {
@@ -220,8 +221,8 @@ __device__ __forceinline__ double spec_core(const NetParams &P, double apow, Net
     return apow * total;                                       // :619
 }
 
-template <class G, bool WIN = true>
-__device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apow, NetSt<G> &s,
+template <class G, bool WIN = true, class RG = Pcg>
+__device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apow, NetSt<G, RG> &s,
                                            const float (&act)[G::E], const double (&Dd)[G::RL], float *orow,
                                            double (&Rn)[G::E], double *met, double *irec) {
     double wa[G::E];
@@ -249,9 +250,9 @@ __device__ __forceinline__ double spec_dyn(const NetParams &P, int t, double apo
 }
 
 // One step (:436-635) at period t < T: the demand draws, then the dynamics
-template <class G>
+template <class G, class RG = Pcg>
 __device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst (&pc)[G::RL], const double *rhs_l,
-                                            int t, double apow, NetSt<G> &s, const float (&act)[G::E],
+                                            int t, double apow, NetSt<G, RG> &s, const float (&act)[G::E],
                                             float *orow, double (&Rn)[G::E], int64_t (&dem)[G::RL],
                                             double *met, double *irec) {
     double Dd[G::RL];
@@ -262,8 +263,8 @@ __device__ __forceinline__ double spec_step(const NetParams &P, const PtrsConst 
 }
 
 // shift the age-aligned windows by one period: age a+1 <- age a, age 1 <- R[t]
-template <class G>
-__device__ __forceinline__ void spec_shift(NetSt<G> &s, const double (&Rn)[G::E]) {
+template <class G, class RG = Pcg>
+__device__ __forceinline__ void spec_shift(NetSt<G, RG> &s, const double (&Rn)[G::E]) {
 #pragma unroll
     for (int k = 0; k < G::E; k++) {
         if (G::L[k] == 0) continue;
@@ -273,7 +274,7 @@ __device__ __forceinline__ void spec_shift(NetSt<G> &s, const double (&Rn)[G::E]
     }
 }
 
-template <class G, bool TU, bool ONE, bool POL>
+template <class G, bool TU, bool ONE, bool POL, class RG>
 __global__ void __launch_bounds__(WAVE)
 net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) float ns_lds[];
@@ -292,7 +293,7 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     double *rhs_l = reinterpret_cast<double *>(ns_lds + ((EPW * O + 3) / 4) * 4);
 
     int t = TU ? t_u : P.cm.period[el];
-    NetSt<G> st;
+    NetSt<G, RG> st;
     if (ONE && TU && t >= P.T) {
         // lock-step NEXT_STEP autoreset of the whole batch (the host refuses a
         // DISABLED overrun when lock-step; SAME_STEP resets in the done step)
@@ -327,7 +328,7 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
 #pragma unroll
         for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
     }
-    st.g = P.cm.rng.load(el);
+    P.cm.rng.load(el, st.g);
 #pragma unroll
     for (int j = 0; j < G::J; j++) st.X[j] = P.X[j * S + el];
 #pragma unroll
@@ -366,6 +367,7 @@ net_spec_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     const int K = ONE ? 1 : io.K;
     for (int kk = 0; kk < K; kk++) {
         const int64_t oi = (int64_t)kk * N + e;
+        st.g.set_step(P.cm.ph_step + (uint64_t)kk);
         if (kk > 0) {
             const int64_t ea = (int64_t)kk * N + el;
             if (!POL) {
@@ -1383,7 +1385,8 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
     const dim3 grid((unsigned)((p.cm.N + EPW - 1) / EPW)), block(WAVE);
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
-    if (p.ahead && net_ahead_enabled() && !pol && io.K == 1 && t_u >= 0 && t_u < p.T && io.obs &&
+    const bool ph = p.cm.philox != 0;       // fast stream: net_spec_kernel only (no lookahead, no demand waves)
+    if (!ph && p.ahead && net_ahead_enabled() && !pol && io.K == 1 && t_u >= 0 && t_u < p.T && io.obs &&
         !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.T)) {
         const bool hit = ahead;
         const int gla = hit ? (int)((p.cm.N + WAVE - 1) / WAVE) : 0;
@@ -1408,8 +1411,12 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
         ahead = false;
         if (ce != hipSuccess) return ce;
     }
-#define K_(TU, ONE, POL) hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
-    if (!pol && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
+#define K_(TU, ONE, POL)                                                                                   \
+    do {                                                                                                   \
+        if (ph) hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL, PhiloxGen>), grid, block, lds, s, p, t_u, io, pv); \
+        else hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL, Pcg>), grid, block, lds, s, p, t_u, io, pv);         \
+    } while (0)
+    if (!ph && !pol && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
         (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
         const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE));
         if (net_roll3_use(p.cm.N)) {

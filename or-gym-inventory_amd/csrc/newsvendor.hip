@@ -51,9 +51,9 @@ __device__ __forceinline__ double np_clip(double x, double lo, double hi) {
     return (y > hi) ? hi : y;
 }
 
-template <int LT>
+template <int LT, class G = Pcg>
 struct NvState {
-    Pcg g;
+    G g;
     double par[5];                 // price, cost, h, k, mu
     float pv[(LT > 0) ? LT : 1];   // pipeline positions 0 (arriving) .. L-1 (newest)
 };
@@ -64,9 +64,10 @@ __device__ __forceinline__ void obs_params(const double *par, float *orow) {
 }
 
 // newsvendor.py:100-123: 5 uniforms, params, empty pipeline, obs row
-template <int LT>
-__device__ __forceinline__ void nv_reset_regs(const NvParams &P, int64_t e, NvState<LT> &s, float *orow,
+template <int LT, class G = Pcg>
+__device__ __forceinline__ void nv_reset_regs(const NvParams &P, int64_t e, NvState<LT, G> &s, float *orow,
                                               bool leader) {
+    s.g.sub(PhiloxGen::RESET);                          // fast stream: the reset's own counter block
     double price = s.g.next_double() * P.p_max;
     if (!(price > 1)) price = 1;                        // max(1, x)
     double cost = s.g.next_double() * price;
@@ -91,8 +92,8 @@ __device__ __forceinline__ void nv_reset_regs(const NvParams &P, int64_t e, NvSt
 
 // Sum of the pipeline as the observation holds it (float32, numpy pairwise
 // order): observation[5:].sum()
-template <int LT>
-__device__ __forceinline__ float nv_pipe_sum(const NvParams &P, int64_t e, int sc, const NvState<LT> &s) {
+template <int LT, class G = Pcg>
+__device__ __forceinline__ float nv_pipe_sum(const NvParams &P, int64_t e, int sc, const NvState<LT, G> &s) {
     const int64_t S = P.cm.Npad;
     const int L = (LT >= 0) ? LT : P.L;
     const int base = (L > 0) ? (int)((uint32_t)(sc + 1) % (uint32_t)L) : 0;
@@ -107,9 +108,9 @@ __device__ __forceinline__ float nv_pipe_sum(const NvParams &P, int64_t e, int s
 // OrderUpToHeuristicAgent.get_action (benchmark_newsvendor.py:103-111), float32
 // as numpy evaluates it: target = mu * (L + 1) * sf, order max(0, target -
 // pipeline.sum()) clipped to the action space [0, max_order_quantity]
-template <int LT>
+template <int LT, class G = Pcg>
 __device__ __forceinline__ float nv_order_up_to(const NvParams &P, const PolicyIO &pol, int64_t e, int sc,
-                                                const NvState<LT> &s) {
+                                                const NvState<LT, G> &s) {
     const int L = (LT >= 0) ? LT : P.L;
     const float mu = (float)s.par[4];                                  // observation[4]
     const float target = (mu * (float)(L + 1)) * (float)pol.sf;
@@ -232,9 +233,9 @@ __device__ double nv_poisson_ppf(double q, double lam, bool single) {
 // the critical ratio and the effective mean are float32, poisson.ppf returns
 // float64, and the order is clipped in float64 and cast to float32.  The ppf
 // level depends only on the episode's params: computed once per episode (lvl).
-template <int LT>
+template <int LT, class G = Pcg>
 __device__ __forceinline__ float nv_classic(const NvParams &P, const PolicyIO &pol, int64_t e, int sc,
-                                            const NvState<LT> &s, double &lvl, bool &have) {
+                                            const NvState<LT, G> &s, double &lvl, bool &have) {
     const int L = (LT >= 0) ? LT : P.L;
     const float price = (float)s.par[0], cost = (float)s.par[1], h = (float)s.par[2], k = (float)s.par[3],
                 mu = (float)s.par[4];
@@ -274,9 +275,9 @@ __device__ __forceinline__ float nv_classic(const NvParams &P, const PolicyIO &p
 // module's last definition): s = ppf(clip(k / (h + k), 0.001, 0.999), mu (L + 1))
 // in float32 inputs, S = s * S_buffer_factor; order up to S when the pipeline is
 // below s.  The level s is per episode (lvl).
-template <int LT>
+template <int LT, class G = Pcg>
 __device__ __forceinline__ float nv_ss(const NvParams &P, const PolicyIO &pol, int64_t e, int sc,
-                                       const NvState<LT> &s, double &lvl, bool &have) {
+                                       const NvState<LT, G> &s, double &lvl, bool &have) {
     const int L = (LT >= 0) ? LT : P.L;
     if (!have) {
         const float h = (float)s.par[2], k = (float)s.par[3], mu = (float)s.par[4];
@@ -307,8 +308,8 @@ __device__ __forceinline__ float nv_ss(const NvParams &P, const PolicyIO &pol, i
 }
 
 // One newsvendor.py:125-204 step at step count sc.  Returns truncated.
-template <int LT>
-__device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool valid, int sc, NvState<LT> &s,
+template <int LT, class G = Pcg>
+__device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool valid, int sc, NvState<LT, G> &s,
                                              float action, float *orow, const double *lg_l, TableStage *ts,
                                              double &reward, int64_t *dem, int64_t dpre = -1,
                                              double *irec = nullptr) {
@@ -324,6 +325,7 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
     if (ts) ts->flush((int)threadIdx.x);
     TPROBE(1);
     // :146 (dpre >= 0: drawn by the previous launch's lookahead, nv_step1_kernel)
+    if (dpre < 0) s.g.sub(0);
     const int64_t d = dpre >= 0 ? dpre : env_poisson_dyn(s.g, s.par[4], lg_l, RHS_LDS_MAX);
     TPROBE(2);
     const Tv ZERO = tv(0.0, K_PY);
@@ -370,7 +372,7 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
     return sc + 1 >= P.step_limit;                                          // :190
 }
 
-template <int LT, bool TU, bool ONE, bool POL>
+template <int LT, bool TU, bool ONE, bool POL, class G>
 __global__ void __launch_bounds__(WAVE)
 nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) float nv_tile[];
@@ -393,8 +395,9 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     // the Poisson loop finite
     const int64_t el = valid ? e : N - 1;
 
-    NvState<LT> st;
-    st.g = P.cm.rng.load(el);
+    NvState<LT, G> st;
+    P.cm.rng.load(el, st.g);
+    st.g.set_step(P.cm.ph_step);
     int sc = TU ? t_u : P.cm.period[el];
     if (ONE && TU && sc >= P.step_limit && P.cm.autoreset == AR_NEXT_STEP) {
         // lock-step NEXT_STEP autoreset of the whole batch.  DISABLED keeps stepping
@@ -441,6 +444,7 @@ nv_run_kernel(NvParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     for (int k = 0; k < K; k++) {
         const int64_t oi = (int64_t)k * N + e;
         float act;
+        st.g.set_step(P.cm.ph_step + (uint64_t)k);
         if (!POL) act = io.act[(int64_t)k * N + el];
         if (!(ONE && TU) && P.cm.autoreset == AR_NEXT_STEP && sc >= P.step_limit) {
             nv_reset_regs<LT>(P, e, st, trow, valid);
@@ -1109,10 +1113,18 @@ nv_reset_kernel(NvParams P, const uint8_t *__restrict__ mask, float *__restrict_
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= P.cm.N) return;
     if (mask && !mask[e]) return;
-    NvState<-1> st;
-    st.g = P.cm.rng.load(e);
-    nv_reset_regs<-1>(P, e, st, obs ? obs + e * (P.L + 5) : nullptr, true);
-    P.cm.rng.store_state(e, st.g);
+    float *orow = obs ? obs + e * (P.L + 5) : nullptr;
+    if (P.cm.philox) {
+        NvState<-1, PhiloxGen> st;
+        P.cm.rng.load(e, st.g);
+        st.g.set_step(P.cm.ph_step);
+        nv_reset_regs<-1>(P, e, st, orow, true);
+    } else {
+        NvState<-1> st;
+        st.g = P.cm.rng.load(e);
+        nv_reset_regs<-1>(P, e, st, orow, true);
+        P.cm.rng.store_state(e, st.g);
+    }
     P.cm.period[e] = 0;
 }
 
@@ -1151,7 +1163,8 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
-    const bool la = p.ahead && nv_ahead_enabled();
+    const bool ph = p.cm.philox != 0;       // fast stream: the run kernels only (no lookahead, no stream waves)
+    const bool la = p.ahead && nv_ahead_enabled() && !ph;
     if (la && !pol && io.K == 1 && t_u >= 0 && t_u < p.step_limit && io.obs &&
         !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.step_limit)) {
         const bool produce = t_u + 1 < p.step_limit;
@@ -1182,7 +1195,7 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
         ahead = false;
         if (ce != hipSuccess) return ce;
     }
-    if (!pol && io.K > 1 && t_u >= 0 && p.L > 0 && p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
+    if (!ph && !pol && io.K > 1 && t_u >= 0 && p.L > 0 && p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
         const dim3 gr(grid_for(p.cm.N, WAVE)), br(3 * WAVE);
         bool done = true;
 #define R_(X)                                                                                              \
@@ -1194,8 +1207,11 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
 #undef R_
         if (done) return hipGetLastError();
     }
-#define K_(X, TU, ONE, POL) \
-    hipLaunchKernelGGL((nv_run_kernel<X, TU, ONE, POL>), grid, block, lds, s, p, t_u, io, pv)
+#define K_(X, TU, ONE, POL)                                                                              \
+    do {                                                                                                 \
+        if (ph) hipLaunchKernelGGL((nv_run_kernel<X, TU, ONE, POL, PhiloxGen>), grid, block, lds, s, p, t_u, io, pv); \
+        else hipLaunchKernelGGL((nv_run_kernel<X, TU, ONE, POL, Pcg>), grid, block, lds, s, p, t_u, io, pv);         \
+    } while (0)
 #define L_(X)                                          \
     do {                                               \
         if (pol) {                                     \

@@ -32,7 +32,8 @@ struct NpDist {
 };
 
 // pcg64_next32: low half first, high half buffered (bit 32 of buf = has_uint32)
-__device__ __forceinline__ uint32_t np_next32(Pcg &g, uint64_t &buf) {
+template <class G>
+__device__ __forceinline__ uint32_t np_next32(G &g, uint64_t &buf) {
     if (buf >> 32) {
         const uint32_t v = (uint32_t)buf;
         buf = 0;
@@ -43,7 +44,8 @@ __device__ __forceinline__ uint32_t np_next32(Pcg &g, uint64_t &buf) {
     return (uint32_t)x;
 }
 
-__device__ inline int64_t np_integers(Pcg &g, uint64_t &buf, const NpDist &d) {
+template <class G>
+__device__ inline int64_t np_integers(G &g, uint64_t &buf, const NpDist &d) {
     const uint64_t r = d.rng;
     if (r == 0) return (int64_t)d.off;
     if (r <= 0xFFFFFFFFull) {
@@ -75,7 +77,8 @@ __device__ inline int64_t np_integers(Pcg &g, uint64_t &buf, const NpDist &d) {
     return (int64_t)(d.off + hi);
 }
 
-__device__ inline int64_t np_binomial_inversion(Pcg &g, const NpDist &d) {
+template <class G>
+__device__ inline int64_t np_binomial_inversion(G &g, const NpDist &d) {
     const int64_t n = d.n;
     const double p = d.p, q = d.q, qn = d.qn;
     int64_t X = 0;
@@ -95,7 +98,8 @@ __device__ inline int64_t np_binomial_inversion(Pcg &g, const NpDist &d) {
     return X;
 }
 
-__device__ inline int64_t np_binomial_btpe(Pcg &g, const NpDist &d) {
+template <class G>
+__device__ inline int64_t np_binomial_btpe(G &g, const NpDist &d) {
     const int64_t n = d.n, m = d.m;
     const double r = d.r, q = d.q, xm = d.xm, xl = d.xl, xr = d.xr, c = d.c, laml = d.laml, lamr = d.lamr;
     const double p1 = d.p1, p2 = d.p2, p3 = d.p3, p4 = d.p4;
@@ -150,13 +154,15 @@ __device__ inline int64_t np_binomial_btpe(Pcg &g, const NpDist &d) {
     }
 }
 
-__device__ inline int64_t np_binomial(Pcg &g, const NpDist &d) {
+template <class G>
+__device__ inline int64_t np_binomial(G &g, const NpDist &d) {
     if (d.zero) return 0;
     const int64_t X = d.inversion ? np_binomial_inversion(g, d) : np_binomial_btpe(g, d);
     return d.flip ? d.n - X : X;
 }
 
-__device__ inline double np_standard_exponential(Pcg &g) {
+template <class G>
+__device__ inline double np_standard_exponential(G &g) {
     for (;;) {
         uint64_t ri = g.next64();
         ri >>= 3;
@@ -169,7 +175,8 @@ __device__ inline double np_standard_exponential(Pcg &g) {
     }
 }
 
-__device__ inline int64_t np_geometric(Pcg &g, const NpDist &d) {
+template <class G>
+__device__ inline int64_t np_geometric(G &g, const NpDist &d) {
     if (d.inversion) {                                   // search, p >= 1/3
         int64_t X = 1;
         double sum = d.p, prod = d.p;
@@ -186,7 +193,8 @@ __device__ inline int64_t np_geometric(Pcg &g, const NpDist &d) {
     return (int64_t)z;
 }
 
-__device__ __forceinline__ int64_t np_demand(Pcg &g, uint64_t &buf, const NpDist &d) {
+template <class G>
+__device__ __forceinline__ int64_t np_demand(G &g, uint64_t &buf, const NpDist &d) {
     if (d.kind == 2) return np_binomial(g, d);
     if (d.kind == 3) return np_integers(g, buf, d);
     return np_geometric(g, d);

@@ -26,8 +26,9 @@ EXPORTS = (
     "invsim_rollout_policy", "invsim_info_record_dim", "invsim_set_info_record", "invsim_set_info_demand",
     "invsim_state_bytes",
     "invsim_state_field", "invsim_get_state", "invsim_set_state", "invsim_episode_fold",
-    "invsim_debug_ptrs_stats",
+    "invsim_debug_ptrs_stats", "invsim_set_demand_stream", "invsim_demand_stream",
 )
+DEMAND_STREAMS = {"numpy": 0, "philox": 1}
 
 
 class NewsvendorSpec(C.Structure):
@@ -102,6 +103,8 @@ def _declare(lib):
         "invsim_set_state": ([H, P, P], C.c_int),
         "invsim_episode_fold": ([P, P, P, I32, I64, P, P, P], C.c_int),
         "invsim_debug_ptrs_stats": ([P, I32], C.c_int),
+        "invsim_set_demand_stream": ([H, I32], C.c_int),
+        "invsim_demand_stream": ([H, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

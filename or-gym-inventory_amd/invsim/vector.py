@@ -18,6 +18,11 @@ Autoreset modes (``gymnasium.vector.AutoresetMode``):
 * ``"disabled"``: the caller resets; stepping an InvMgmt/NetInvMgmt env past
   its horizon raises IndexError as the reference does
   (``inventory_management.py:267``).
+
+Demand stream (``demand_stream=``): ``"numpy"`` (default) draws from numpy's
+PCG64 Generator stream, bit-exact with the reference on the same seeds;
+``"philox"`` is the opt-in, non-parity fast stream (rocRAND Philox4x32-10,
+counter-based: no per-env generator state per step; ``include/invsim.h``).
 """
 import os
 
@@ -67,7 +72,7 @@ class InvSimVectorEnv:
     act_dtype = torch.float32
 
     def __init__(self, num_envs, device=None, autoreset_mode="next_step", global_offset=0,
-                 record_demand=False, record_info=False, copy=True):
+                 record_demand=False, record_info=False, copy=True, demand_stream="numpy"):
         if not torch.cuda.is_available():
             raise RuntimeError("invsim requires a ROCm GPU (torch.cuda.is_available() is False); "
                                "there is no CPU fallback")
@@ -88,6 +93,7 @@ class InvSimVectorEnv:
         self.obs_dim, self.action_dim, self.demand_dim = od.value, ad.value, dd.value
         self.observation_space = batch_box(self.single_observation_space, self.num_envs)
         self.action_space = batch_box(self.single_action_space, self.num_envs)
+        self.set_demand_stream(demand_stream)
         self._seeded = False
         self._demand = None
         if record_demand:
@@ -281,6 +287,20 @@ class InvSimVectorEnv:
         f = _capi.C.c_uint32()
         _capi.check(self._lib.invsim_status(self._h, _capi.C.byref(f), int(clear)), self._h, "status")
         return f.value
+
+    def set_demand_stream(self, mode):
+        """"numpy" (parity, default) or "philox" (fast, NOT the reference's draws)."""
+        if mode not in _capi.DEMAND_STREAMS:
+            raise ValueError(f"demand_stream must be one of {sorted(_capi.DEMAND_STREAMS)}")
+        _capi.check(self._lib.invsim_set_demand_stream(self._h, _capi.DEMAND_STREAMS[mode]), self._h,
+                    "set_demand_stream")
+
+    @property
+    def demand_stream(self):
+        """The stream the handle draws demands from ("numpy" or "philox")."""
+        m = _capi.C.c_int32()
+        _capi.check(self._lib.invsim_demand_stream(self._h, _capi.C.byref(m)), self._h, "demand_stream")
+        return {v: k for k, v in _capi.DEMAND_STREAMS.items()}[m.value]
 
     @property
     def kernel_variant(self):

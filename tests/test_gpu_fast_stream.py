@@ -1,0 +1,151 @@
+"""The opt-in fast demand stream (demand_stream="philox", include/invsim.h
+INVSIM_DEMAND_PHILOX): rocRAND Philox4x32-10 used counter-based with numpy's
+PTRS / multiplication transforms.  It is NOT the reference's stream, so parity
+is replaced by statistics: a chi-square goodness-of-fit against the Poisson
+pmf over >= 1e8 draws per rate (both sampler branches and the boundary
+lam = 10), plus the stream's own contracts (opt-in, rollout == steps,
+checkpoint round trip, the PCG64 states untouched)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fast_stream_is_opt_in(gpu):
+    import invsim
+    env = invsim.InvManagementBacklogEnv(256, device=gpu, record_demand=True)
+    assert env.demand_stream == "numpy"
+    env.reset(seed=3)
+    a = torch.full((256, 3), 10, dtype=torch.int64, device=gpu)
+    d_np = env.step(a)[4]["demand"].clone()
+    env2 = invsim.InvManagementBacklogEnv(256, device=gpu, record_demand=True, demand_stream="philox")
+    assert env2.demand_stream == "philox"
+    env2.reset(seed=3)
+    d_ph = env2.step(a)[4]["demand"].clone()
+    assert not torch.equal(d_np, d_ph)
+    with pytest.raises(ValueError):
+        env.set_demand_stream("rocrand-xorwow")
+
+
+def _chi2_poisson(counts, lam, n):
+    from scipy.stats import chi2, poisson
+    k = np.arange(len(counts))
+    p = poisson.pmf(k, lam)
+    p[-1] += poisson.sf(len(counts) - 1, lam)         # the last bin takes the upper tail
+    exp = p * n
+    # pool bins with expected count < 50 into their neighbours (both tails)
+    obs_b, exp_b = [], []
+    o_acc = e_acc = 0.0
+    for o, e in zip(counts, exp):
+        o_acc += o
+        e_acc += e
+        if e_acc >= 50:
+            obs_b.append(o_acc)
+            exp_b.append(e_acc)
+            o_acc = e_acc = 0.0
+    if e_acc > 0:
+        obs_b[-1] += o_acc
+        exp_b[-1] += e_acc
+    obs_b, exp_b = np.array(obs_b), np.array(exp_b)
+    stat = float(((obs_b - exp_b) ** 2 / exp_b).sum())
+    dof = len(obs_b) - 1
+    return stat, dof, float(chi2.sf(stat, dof))
+
+
+@pytest.mark.parametrize("lam", [0.3, 5.0, 9.99, 10.0, 20.0, 162.65])
+def test_fast_stream_poisson_chi_square_1e8(gpu, lam):
+    import invsim
+    n, cycles = 65536, 51                        # 51 episodes x 30 draws x 65 536 envs = 1.003e8
+    env = invsim.InvManagementLostSalesEnv(n, device=gpu, dist_param={"mu": lam}, record_demand=True,
+                                           demand_stream="philox", copy=False)
+    env.reset(seed=11)
+    a = torch.zeros((n, 3), dtype=torch.int64, device=gpu)
+    hi = int(lam + 12 * np.sqrt(lam) + 30)
+    counts = torch.zeros(hi + 1, dtype=torch.int64, device=gpu)
+    s1 = torch.zeros((), dtype=torch.float64, device=gpu)
+    lag = torch.zeros((), dtype=torch.float64, device=gpu)
+    prev = None
+    draws = 0
+    for k in range(31 * cycles):
+        _, _, _, tr, info = env.step(a)
+        if k % 31 == 30:                         # the NEXT_STEP reset call draws nothing
+            prev = None
+            continue
+        d = info["demand"]
+        counts += torch.bincount(d.clamp(max=hi), minlength=hi + 1)
+        s1 += d.sum(dtype=torch.float64)
+        if prev is not None:
+            lag += (d.double() * prev.double()).sum()
+        prev = d
+        draws += n
+    assert draws >= 100_000_000
+    c = counts.cpu().numpy().astype(np.float64)
+    stat, dof, p = _chi2_poisson(c, lam, draws)
+    assert p > 1e-4, f"chi-square {stat:.1f} on {dof} dof, p = {p:.2e}"
+    mean = float(s1) / draws
+    assert abs(mean - lam) < 6 * np.sqrt(lam / draws)
+    # consecutive steps of an env are uncorrelated: E[d_t d_t+1] = lam^2
+    pairs = (31 - 2) * cycles * n
+    assert abs(float(lag) / pairs - lam * lam) < 6 * lam * np.sqrt((1 + 2 * lam) / pairs) + 1e-12
+
+
+def test_fast_stream_rollout_equals_steps_and_keeps_pcg_states(gpu):
+    import invsim
+    n, K = 4096, 70
+    mk = lambda: invsim.InvManagementBacklogEnv(n, device=gpu, demand_stream="philox")  # noqa: E731
+    e1, e2 = mk(), mk()
+    e1.reset(seed=5)
+    e2.reset(seed=5)
+    rng0 = e1.state_fields()["rng"].clone()
+    g = torch.Generator(device=gpu)
+    g.manual_seed(1)
+    acts = torch.randint(0, 90, (K, n, 3), device=gpu, generator=g)
+    o1, r1, _, t1 = e1.rollout(acts)
+    for k in range(K):
+        o, r, _, t, _ = e2.step(acts[k])
+        assert torch.equal(o, o1[k]) and torch.equal(r, r1[k]) and torch.equal(t, t1[k]), k
+    assert torch.equal(e1.state_fields()["rng"], rng0)          # the parity stream is untouched
+
+
+@pytest.mark.parametrize("cls", ["NewsvendorEnv", "NetInvMgmtBacklogEnv", "InvManagementBacklogEnv"])
+def test_fast_stream_checkpoint_round_trip(gpu, cls):
+    import invsim
+    n = 1000
+    env = getattr(invsim, cls)(n, device=gpu, demand_stream="philox")
+    env.reset(seed=9)
+    A = env.action_dim
+    dt = env.act_dtype
+    a = (torch.ones((n, A), device=gpu) * 20).to(dt)
+    for _ in range(7):
+        env.step(a)
+    blob = env.get_state().clone()
+    ref = [env.step(a)[:2] for _ in range(40)]
+    env2 = getattr(invsim, cls)(n, device=gpu, demand_stream="philox")
+    env2.set_state(blob)
+    for k in range(40):
+        o, r = env2.step(a)[:2]
+        assert torch.equal(o, ref[k][0]) and torch.equal(r.view(torch.int64), ref[k][1].view(torch.int64)), k
+
+
+def test_fast_stream_newsvendor_and_net_rates(gpu):
+    """Newsvendor: demand ~ Poisson(mu) with mu ~ U(0, mu_max) per episode, so
+    E[d] = mu_max / 2; Net default graph: one market, Poisson(20)."""
+    import invsim
+    n = 65536
+    nv = invsim.NewsvendorEnv(n, device=gpu, record_demand=True, demand_stream="philox")
+    nv.reset(seed=1)
+    a = torch.zeros((n, 1), device=gpu)
+    tot, cnt = 0.0, 0
+    for k in range(41 * 4):
+        d = nv.step(a)[4]["demand"]
+        if k % 41 != 40:
+            tot += float(d.sum())
+            cnt += n
+    assert abs(tot / cnt - 100.0) < 1.0
+    net = invsim.NetInvMgmtBacklogEnv(32768, device=gpu, record_demand=True, demand_stream="philox")
+    net.reset(seed=2)
+    a = torch.zeros((32768, net.action_dim), device=gpu)
+    ds = torch.stack([net.step(a)[4]["demand"].double() for _ in range(30)])
+    assert abs(float(ds.mean()) - 20.0) < 0.05
+    assert abs(float(ds.var()) - 20.0) < 0.5
