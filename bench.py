@@ -182,9 +182,9 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     """Warm up, then time `steps` env.step()s of the whole batch (mode "step":
     one invsim_step each; "rollout": invsim_rollout launches of K steps), with
     barrier + synchronize on both sides and the max over ranks.  The step
-    outputs are written into a [R, N] slab that the HIP episode fold
-    (invsim_episode_fold) reduces every R steps inside the timed region; the
-    statistics are all-reduced once after it."""
+    outputs are written into [R, N] slabs that the HIP episode fold
+    (invsim_episode_fold) reduces every R steps inside the timed region, on a
+    side stream; the statistics are all-reduced once after it."""
     import torch
     import invsim
     from invsim.distributed import EpisodeStats
@@ -197,17 +197,28 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     acts = make_actions(env, pool, K, gen)
     ptrs = [a.data_ptr() for a in acts]
     R = K if K else 32                              # slab rows = steps per fold
-    rew = torch.empty((R, N), dtype=torch.float64, device=dev)
-    term = torch.empty((R, N), dtype=torch.bool, device=dev)
-    trunc = torch.empty((R, N), dtype=torch.bool, device=dev)
+    # two output slabs: the fold of one runs on a side stream while the steps
+    # write the other (events order slab reuse), so the reduction overlaps the
+    # env kernels instead of sitting between them
+    rew = torch.empty((2, R, N), dtype=torch.float64, device=dev)
+    term = torch.empty((2, R, N), dtype=torch.bool, device=dev)
+    trunc = torch.empty((2, R, N), dtype=torch.bool, device=dev)
     obs = torch.empty(((K or 1), N, O), dtype=env.obs_dtype, device=dev)
-    po, pr, pt, pu = obs.data_ptr(), rew.data_ptr(), term.data_ptr(), trunc.data_ptr()
+    po = obs.data_ptr()
+    slab_ptrs = [(rew[b].data_ptr(), term[b].data_ptr(), trunc[b].data_ptr()) for b in range(2)]
     stats = EpisodeStats(N, dev)
+    fstream = torch.cuda.Stream(dev)
+    fsp = fstream.cuda_stream
+    ev_out = [torch.cuda.Event() for _ in range(2)]     # slab written (kernel stream)
+    ev_free = [torch.cuda.Event() for _ in range(2)]    # slab folded (side stream)
+    for ev in ev_out + ev_free:
+        ev.record(stream)
     if mode == "step":
         step_fn = lib.invsim_step
         calls_per_block = R
 
-        def one(i, row):
+        def one(i, row, sl):
+            pr, pt, pu = slab_ptrs[sl]
             rc = step_fn(h, ptrs[i % pool], po, pr + 8 * row * N, pt + row * N, pu + row * N, None, sp)
             if rc:
                 raise RuntimeError(invsim._capi.last_error(h))
@@ -216,7 +227,8 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
         fn = lib.invsim_rollout
         calls_per_block = 1
 
-        def one(i, row):
+        def one(i, row, sl):
+            pr, pt, pu = slab_ptrs[sl]
             rc = fn(h, K, ptrs[i % pool], po, pr, pt, pu, sp)
             if rc:
                 raise RuntimeError(invsim._capi.last_error(h))
@@ -226,28 +238,33 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     calls = max(1, steps // steps_per_call)
     warm = max(1, warmup // steps_per_call)
     nblocks = (calls + calls_per_block - 1) // calls_per_block
-    # HIP events on the kernel stream around each block of launches (the fold
-    # runs between blocks, outside the event pairs): sum of the pairs / launches
-    # is the mean launch duration.  torch creates an event at its first record:
-    # record every event once here, so creation stays out of the timed region.
+    # HIP events on the kernel stream around each block of launches: sum of the
+    # pairs / launches is the mean launch duration.  torch creates an event at
+    # its first record: record every event once here, so creation stays out of
+    # the timed region.
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nblocks)]
     for a, b in evs:
         a.record(stream)
         b.record(stream)
+    blk = [0]
 
     def region(n_calls, timed):
-        done = 0
         for bi in range(0, n_calls, calls_per_block):
             nb = min(calls_per_block, n_calls - bi)
+            sl = blk[0] & 1
+            stream.wait_event(ev_free[sl])              # this slab's previous fold is done
             if timed:
                 evs[bi // calls_per_block][0].record(stream)
             for j in range(nb):
-                one(bi + j, j * (rows_per_call if K == 0 else 0))
+                one(bi + j, j * (rows_per_call if K == 0 else 0), sl)
             if timed:
                 evs[bi // calls_per_block][1].record(stream)
-            _fold_rows(stats, rew, term, trunc, nb * rows_per_call if K == 0 else K, sp)
-            done += nb
-        return done
+            ev_out[sl].record(stream)
+            fstream.wait_event(ev_out[sl])
+            rows = nb * rows_per_call if K == 0 else K
+            _fold_rows(stats, rew[sl], term[sl], trunc[sl], rows, fsp)
+            ev_free[sl].record(fstream)
+            blk[0] += 1
 
     region(warm, False)
     torch.cuda.synchronize(dev)

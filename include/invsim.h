@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define INVSIM_ABI_VERSION 1
+#define INVSIM_ABI_VERSION 2   /* 2: market samplers appended to invsim_netinvmgmt_spec */
 
 #define INVSIM_OK 0
 #define INVSIM_EINVAL (-22)
@@ -132,6 +132,15 @@ typedef struct {
     const int32_t *succ_idx;        /* [succ_ptr[J]] */
     const int32_t *pred_ptr;        /* [J+1] */
     const int32_t *pred_idx;        /* [pred_ptr[J]] */
+    /* market demand samplers per retail link, the numpy Generator method the
+     * edge's demand_dist_func calls with dist_param (network_management.py:
+     * 125-127, 257-263; demand = max(0, int(round(draw)))).  rl_dist NULL = all
+     * Poisson(rl_lam).  1 poisson(rl_lam), 2 binomial(rl_n, rl_dp),
+     * 3 integers(rl_n, rl_high) (high exclusive), 4 geometric(rl_dp).  Graphs
+     * with a non-Poisson market run the generic kernel. */
+    const int32_t *rl_dist;
+    const int64_t *rl_n, *rl_high;
+    const double *rl_dp;
 } invsim_netinvmgmt_spec;
 
 int invsim_abi_version(void);

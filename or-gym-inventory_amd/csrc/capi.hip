@@ -509,8 +509,19 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
     for (int r = 0; r < RL; r++) {
         if (s->rl_node[r] < 0 || s->rl_node[r] >= J) return fail(nullptr, INVSIM_EINVAL, "retail link node out of range");
         if (!(s->rl_p[r] >= 0) || !(s->rl_b[r] >= 0)) return fail(nullptr, INVSIM_EINVAL, "Invalid or missing p/b>=0");
-        if (!s->rl_user[r] && (!(s->rl_lam[r] >= 0) || s->rl_lam[r] > 1e18))
-            return fail(nullptr, INVSIM_EINVAL, "poisson lam out of range");
+        const int dk = s->rl_dist ? s->rl_dist[r] : 1;
+        if (!s->rl_user[r]) {
+            if (dk < 1 || dk > 4) return fail(nullptr, INVSIM_EINVAL, "market sampler must be 1..4");
+            if (dk == 1 && (!(s->rl_lam[r] >= 0) || s->rl_lam[r] > 1e18))
+                return fail(nullptr, INVSIM_EINVAL, "poisson lam out of range");
+            if (dk > 1 && (!s->rl_n || !s->rl_high || !s->rl_dp)) return fail(nullptr, INVSIM_EINVAL, "null market sampler table");
+            if (dk == 2 && (s->rl_n[r] < 0 || !(s->rl_dp[r] >= 0 && s->rl_dp[r] <= 1)))
+                return fail(nullptr, INVSIM_EINVAL, "binomial market needs n >= 0 and 0 <= p <= 1");
+            if (dk == 3 && !(s->rl_high[r] > s->rl_n[r]))
+                return fail(nullptr, INVSIM_EINVAL, "integers market: low >= high");
+            if (dk == 4 && !(s->rl_dp[r] > 0 && s->rl_dp[r] <= 1))
+                return fail(nullptr, INVSIM_EINVAL, "geometric market needs 0 < p <= 1");
+        }
         if (s->rl_user[r] && !s->user_D) return fail(nullptr, INVSIM_EINVAL, "user_D table missing");
     }
     const int nsucc = s->succ_ptr[J], npred = s->pred_ptr[J];
@@ -540,6 +551,19 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
     int64_t o_U = lay.add("U", 8, std::max(RL, 1), h->Npad);
     int64_t o_Y = lay.add("Y", 8, std::max(E, 1), h->Npad);
     int64_t o_R = lay.add("Rring", 8, std::max(sumL, 1), h->Npad);
+    bool any_int = false, any_npd = false;
+    std::vector<int32_t> rdist((size_t)std::max(RL, 1), 1);
+    std::vector<NpDist> rnd((size_t)std::max(RL, 1));
+    for (int r = 0; r < RL; r++) {
+        rdist[r] = (s->rl_dist && !s->rl_user[r]) ? s->rl_dist[r] : 1;
+        if (rdist[r] == 2) rnd[r] = np_dist_binomial(s->rl_n[r], s->rl_dp[r]);
+        if (rdist[r] == 3) rnd[r] = np_dist_integers(s->rl_n[r], s->rl_high[r] - 1);
+        if (rdist[r] == 4) rnd[r] = np_dist_geometric(s->rl_dp[r]);
+        any_int = any_int || rdist[r] == 3;
+        any_npd = any_npd || rdist[r] > 1;
+    }
+    // numpy's buffered 32-bit half of the bit generator (integers markets only)
+    const int64_t o_U32 = any_int ? lay.add("u32buf", 8, 1, h->Npad) : -1;
     Blob tb;
     int64_t t_I0 = tb.put(s->I0, J), t_h = tb.put(s->h, J), t_C = tb.put(s->C, J),
             t_o = tb.put(s->o, J), t_v = tb.put(s->v, J);
@@ -568,6 +592,7 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
     }
     int64_t t_pc = tb.put(pcs.data(), pcs.size());
     int64_t t_rhs = tb.put(rhs.data(), rhs.size());
+    int64_t t_rd = tb.put(rdist.data(), rdist.size()), t_rnd = tb.put(rnd.data(), rnd.size());
     std::vector<double> ud((size_t)std::max(RL, 1) * s->num_periods, 0.0);
     if (s->user_D) std::memcpy(ud.data(), s->user_D, sizeof(double) * RL * s->num_periods);
     int64_t t_ud = tb.put(ud.data(), ud.size());
@@ -616,6 +641,10 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
         p.rl_p = tab<double>(h, t_rp);
         p.rl_b = tab<double>(h, t_rb);
         p.rl_pc = tab<PtrsConst>(h, t_pc);
+        p.rl_dist = any_npd ? tab<int32_t>(h, t_rd) : nullptr;
+        p.rl_nd = tab<NpDist>(h, t_rnd);
+        if (o_U32 >= 0) h->cm.u32buf = at<uint64_t>(h, o_U32);
+        p.cm = h->cm;
         p.rhs = rhs.empty() ? nullptr : tab<double>(h, t_rhs);
         p.win_off = tab<int32_t>(h, t_wo);
         p.user_D = tab<double>(h, t_ud);

@@ -121,6 +121,8 @@ struct NetParams {
     const int32_t *rl_node, *rl_user;
     const double *rl_p, *rl_b;
     const PtrsConst *rl_pc;      // [RL]
+    const int32_t *rl_dist;      // [RL] 1 poisson, 2 binomial, 3 integers, 4 geometric (non-Poisson: generic kernel)
+    const NpDist *rl_nd;         // [RL] numpy_dists constants of the non-Poisson markets
     const double *rhs;           // PTRS right-hand-side tables of all retail links (rl_pc[r].toff)
     const double *user_D;        // [RL][T]
     const int32_t *succ_ptr, *succ_kind, *succ_idx, *pred_ptr, *pred_idx;

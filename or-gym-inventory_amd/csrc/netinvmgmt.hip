@@ -58,7 +58,7 @@ __device__ __forceinline__ void net_reset_lds(const NetParams &P, NetScratch &s,
 // LDS scratch, lane-group Poisson draws); lane j == 0 writes state and the
 // U/X part of the obs row, lane j writes the order windows of links k = j mod LPE.
 template <class RG>
-__device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, RG &g, NetScratch &s,
+__device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, RG &g, uint64_t &u32, NetScratch &s,
                              const float *__restrict__ arow, float *orow, double &reward, int64_t *dem,
                              double *irec) {
     const int64_t S = P.cm.Npad;
@@ -74,7 +74,9 @@ __device__ bool net_step_lds(const NetParams &P, int64_t e, int gl, int t, RG &g
         } else {
             const PtrsConst &pc = P.rl_pc[r];
             g.sub((uint32_t)r);                                // fast stream: market r's counter block
-            const int64_t pd = env_poisson(g, pc, P.rhs ? P.rhs + pc.toff : nullptr);
+            const int dk = P.rl_dist ? P.rl_dist[r] : 1;       // the edge's numpy method (:257-263)
+            const int64_t pd = dk == 1 ? env_poisson(g, pc, P.rhs ? P.rhs + pc.toff : nullptr)
+                                       : np_demand(g, u32, P.rl_nd[r]);
             dd = (double)(pd > 0 ? pd : 0);
         }
         LV(s.Dd, r) = dd;
@@ -226,9 +228,11 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     float *trow = tile + (int64_t)(lane / LPE) * O;
 
     RG g;
+    uint64_t u32 = 0;         // numpy's buffered 32-bit half (integers markets)
     int t = t_u;
     if (valid) {
         P.cm.rng.load(e, g);
+        if (P.cm.u32buf && !RG::kCounter) u32 = P.cm.u32buf[e];
         for (int j = 0; j < P.J; j++) LV(s.X, j) = P.X[j * S + e];
         for (int r = 0; r < P.RL; r++) LV(s.U, r) = P.U[r * S + e];
         for (int k = 0; k < P.E; k++) LV(s.Y, k) = P.Y[k * S + e];
@@ -254,7 +258,8 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
                 }
             } else {
                 double r;
-                tr = net_step_lds(P, e, gl, t, g, s, POL ? pol.cf : io.act + oi * P.E, trow, r,
+                if (RG::kCounter) u32 = 0;          // fast stream: no half carried between steps
+                tr = net_step_lds(P, e, gl, t, g, u32, s, POL ? pol.cf : io.act + oi * P.E, trow, r,
                                   k == io.K - 1 ? P.cm.info_demand : nullptr,
                                   k == io.K - 1 ? (double *)P.cm.info_rec : nullptr);
                 if (leader && (!POL || io.rew)) {
@@ -300,6 +305,7 @@ net_run_kernel(NetParams P, int t_u, StepIO<float, float> io, PolicyIO pol) {
     }
     if (valid && leader) {
         P.cm.rng.store_state(e, g);
+        if (P.cm.u32buf && !RG::kCounter) P.cm.u32buf[e] = u32;
         for (int j = 0; j < P.J; j++) P.X[j * S + e] = LV(s.X, j);
         for (int r = 0; r < P.RL; r++) P.U[r * S + e] = LV(s.U, r);
         for (int k = 0; k < P.E; k++) P.Y[k * S + e] = LV(s.Y, k);

@@ -1342,6 +1342,9 @@ static bool topo_eq(const invsim_netinvmgmt_spec &h) {
 }
 
 int net_spec_match(const invsim_netinvmgmt_spec &h) {
+    // the specialised kernels draw Poisson market demand only
+    for (int r = 0; h.rl_dist && r < h.n_retail; r++)
+        if (!h.rl_user[r] && h.rl_dist[r] != 1) return NET_SPEC_NONE;
     if (topo_eq<NetTopoDefault>(h)) return NET_SPEC_DEFAULT;
     if (topo_eq<NetTopoCustom>(h)) return NET_SPEC_CUSTOM;
     return NET_SPEC_NONE;

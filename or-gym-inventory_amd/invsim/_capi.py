@@ -49,7 +49,8 @@ class InvMgmtSpec(C.Structure):
 
 NET_TABLE_FIELDS = ("I0", "h", "C", "o", "v", "is_factory", "is_retail", "sup", "pur",
                     "sup_is_factory", "L", "lp", "lg", "rl_node", "rl_p", "rl_b", "rl_lam",
-                    "rl_user", "user_D", "succ_ptr", "succ_kind", "succ_idx", "pred_ptr", "pred_idx")
+                    "rl_user", "user_D", "succ_ptr", "succ_kind", "succ_idx", "pred_ptr", "pred_idx",
+                    "rl_dist", "rl_n", "rl_high", "rl_dp")
 
 
 class NetInvMgmtSpec(C.Structure):

@@ -69,15 +69,46 @@ def custom_graph(demand_lam=20):
     return g
 
 
-def _demand_lam(attrs):
-    """Demand source of a market link.  The reference stores a sampler lambda
-    (`demand_dist_func`, always numpy poisson in its graphs) plus
-    `dist_param={'lam': ...}` (network_management.py:125-127); only Poisson runs
-    on device."""
-    dp = attrs.get("dist_param", {})
-    if "lam" not in dp:
-        raise ValueError("market link demand must be Poisson: dist_param={'lam': ...}")
-    return float(dp["lam"])
+MARKET_SAMPLERS = {"poisson": 1, "binomial": 2, "integers": 3, "geometric": 4}
+
+
+def market_sampler(attrs):
+    """Demand source of a market link -> (kind, lam, n_or_low, high, p).
+
+    The reference stores a sampler lambda, `demand_dist_func`, called with
+    `dist_param` (network_management.py:125-127, 257-263): numpy poisson in its
+    own graphs, any np_random method in a user's.  The device runs numpy's
+    poisson, binomial, integers and geometric samplers, so the method is read
+    from `demand_dist_func` -- a method name, or the name the lambda's code
+    references (`lambda **p: self.np_random.binomial(**p)`) -- else from the
+    keys of `dist_param`: {lam} poisson, {n, p} binomial, {low[, high]}
+    integers, {p} geometric.  integers(low, high) draws [low, high), and
+    integers(low) [0, low), as numpy's Generator.integers."""
+    f = attrs.get("demand_dist_func")
+    name = f if isinstance(f, str) else None
+    if name is None and f is not None:
+        hit = set(MARKET_SAMPLERS) & set(getattr(getattr(f, "__code__", None), "co_names", ()))
+        if len(hit) != 1:
+            raise ValueError(f"demand_dist_func must call one of np_random.{sorted(MARKET_SAMPLERS)}")
+        name = hit.pop()
+    dp = dict(attrs.get("dist_param", {}))
+    if name is None:
+        keys = set(dp)
+        name = ("poisson" if keys <= {"lam"} else "binomial" if keys == {"n", "p"} else
+                "integers" if keys in ({"low"}, {"low", "high"}) else "geometric" if keys == {"p"} else None)
+    if name not in MARKET_SAMPLERS:
+        raise ValueError(f"unsupported market demand source: {name!r} with dist_param {dp}")
+    try:
+        if name == "poisson":
+            return 1, float(dp.get("lam", 1.0)), 0, 0, 0.0
+        if name == "binomial":
+            return 2, 0.0, int(dp["n"]), 0, float(dp["p"])
+        if name == "integers":
+            lo, hi = (0, int(dp["low"])) if "high" not in dp else (int(dp["low"]), int(dp["high"]))
+            return 3, 0.0, lo, hi, 0.0
+        return 4, 0.0, 0, 0, float(dp["p"])
+    except KeyError as e:
+        raise ValueError(f"{name} market demand needs dist_param {e.args[0]!r}") from None
 
 
 @dataclass
@@ -156,6 +187,10 @@ def compile_graph(g, num_periods, user_D=None, sample_path=None):
     # demand source per market link (network_management.py:240-267)
     lam = np.zeros(len(retail_links), np.float64)
     use = np.zeros(len(retail_links), np.int32)
+    kind = np.ones(max(len(retail_links), 1), np.int32)
+    n_lo = np.zeros(max(len(retail_links), 1), np.int64)
+    high = np.zeros(max(len(retail_links), 1), np.int64)
+    prob = np.zeros(max(len(retail_links), 1), np.float64)
     uD = np.zeros((max(len(retail_links), 1), T), np.float64)
     for e, r in ri.items():
         attrs = g.edges[e]
@@ -168,8 +203,9 @@ def compile_graph(g, num_periods, user_D=None, sample_path=None):
             uD[r] = d
             use[r] = 1
         else:
-            lam[r] = _demand_lam(attrs)
+            kind[r], lam[r], n_lo[r], high[r], prob[r] = market_sampler(attrs)
     t["rl_lam"], t["rl_user"], t["user_D"] = lam, use, uD
+    t["rl_dist"], t["rl_n"], t["rl_high"], t["rl_dp"] = kind, n_lo, high, prob
     sp_, sk, sx, pp, px = [0], [], [], [0], []
     for j in main:
         for k in g.successors(j):

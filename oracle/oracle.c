@@ -830,8 +830,12 @@ typedef struct {
     int32_t *is_factory, *is_retail, *sup, *pur, *L, *sup_is_factory, *rl_node, *rl_user;
     double *lp, *lg, *rl_p, *rl_b, *rl_lam, *user_D;
     int32_t *succ_n, *succ_kind, *succ_idx, *pred_n, *pred_idx;
+    int32_t *rl_dist;
+    int64_t *rl_n, *rl_high;
+    double *rl_dp;
     int64_t n;
     uint64_t *rng;
+    uint32_t *u32; /* per env [2]: the bit generator's buffered 32-bit half (integers markets) */
     double *X, *Y, *R, *S, *U, *D;
     int32_t *period;
 } net_t;
@@ -874,11 +878,18 @@ void *orc_net_create(const orc_net_cfg *cfg, int64_t n) {
     DUP(h->succ_idx, cfg->succ_idx, h->J * ORC_NET_MAXADJ, int32_t);
     DUP(h->pred_n, cfg->pred_n, h->J, int32_t);
     DUP(h->pred_idx, cfg->pred_idx, h->J * ORC_NET_MAXADJ, int32_t);
+    DUP(h->rl_dist, cfg->rl_dist, h->RL, int32_t);
+    if (!cfg->rl_dist)
+        for (int r = 0; r < h->RL; r++) h->rl_dist[r] = 1;
+    DUP(h->rl_n, cfg->rl_n, h->RL, int64_t);
+    DUP(h->rl_high, cfg->rl_high, h->RL, int64_t);
+    DUP(h->rl_dp, cfg->rl_dp, h->RL, double);
     int sumL = 0;
     for (int e = 0; e < h->E; e++) sumL += h->L[e];
     h->O = h->RL + h->J + sumL; /* :188-190 */
     h->n = n;
     h->rng = (uint64_t *)calloc((size_t)n * 4, sizeof(uint64_t));
+    h->u32 = (uint32_t *)calloc((size_t)n * 2, sizeof(uint32_t));
     h->X = (double *)calloc((size_t)n * (h->T + 2) * h->J, sizeof(double));
     h->Y = (double *)calloc((size_t)n * (h->T + 2) * (h->E ? h->E : 1), sizeof(double));
     h->R = (double *)calloc((size_t)n * (h->T + 2) * (h->E ? h->E : 1), sizeof(double));
@@ -896,6 +907,7 @@ void orc_net_destroy(void *p) {
     free(h->sup_is_factory); free(h->lp); free(h->lg); free(h->rl_node); free(h->rl_p);
     free(h->rl_b); free(h->rl_lam); free(h->rl_user); free(h->user_D); free(h->succ_n);
     free(h->succ_kind); free(h->succ_idx); free(h->pred_n); free(h->pred_idx);
+    free(h->rl_dist); free(h->rl_n); free(h->rl_high); free(h->rl_dp); free(h->u32);
     free(h->rng); free(h->X); free(h->Y); free(h->R); free(h->S); free(h->U); free(h->D);
     free(h->period);
     free(h);
@@ -905,7 +917,10 @@ int32_t orc_net_obs_dim(void *p) { return ((net_t *)p)->O; }
 
 void orc_net_seed(void *p, const uint32_t *words, const int32_t *nwords) {
     net_t *h = (net_t *)p;
-    for (int64_t i = 0; i < h->n; i++) orc_seed_pcg64(words + 4 * i, nwords[i], h->rng + 4 * i);
+    for (int64_t i = 0; i < h->n; i++) {
+        orc_seed_pcg64(words + 4 * i, nwords[i], h->rng + 4 * i);
+        h->u32[2 * i] = 0;   /* a new Generator: has_uint32 = 0 */
+    }
 }
 
 #define NX(h, i) ((h)->X + (int64_t)(i) * ((h)->T + 2) * (h)->J)
@@ -1020,8 +1035,14 @@ void orc_net_step(void *p, const float *action, float *obs, double *reward, uint
                 dd = h->user_D[(int64_t)r * h->T + idx];
                 dd = nearbyint(dd);                        /* max(0, int(round(x))) */
                 if (!(dd > 0)) dd = 0.0;
-            } else {
-                int64_t pd = orc_poisson(rng, h->rl_lam[r]);
+            } else {                                       /* max(0, int(round(f(**p)))) :263 */
+                int64_t pd;
+                switch (h->rl_dist[r]) {
+                    case 2: pd = orc_binomial(rng, h->rl_n[r], h->rl_dp[r]); break;
+                    case 3: pd = orc_integers(rng, h->u32 + 2 * i, h->rl_n[r], h->rl_high[r]); break;
+                    case 4: pd = orc_geometric(rng, h->rl_dp[r]); break;
+                    default: pd = orc_poisson(rng, h->rl_lam[r]);
+                }
                 dd = (double)(pd > 0 ? pd : 0);
             }
             D[(int64_t)t * RLs + r] = dd;

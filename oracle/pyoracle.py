@@ -168,7 +168,7 @@ class NetCfg(C.Structure):
         (n, C.c_void_p) for n in ("I0", "h", "C", "o", "v", "is_factory", "is_retail", "sup", "pur",
                                   "L", "sup_is_factory", "lp", "lg", "rl_node", "rl_p", "rl_b",
                                   "rl_lam", "rl_user", "user_D", "succ_n", "succ_kind", "succ_idx",
-                                  "pred_n", "pred_idx")]
+                                  "pred_n", "pred_idx", "rl_dist", "rl_n", "rl_high", "rl_dp")]
 
 
 class _Base:
@@ -370,6 +370,35 @@ def custom_graph():
     return g
 
 
+def market_sampler(attrs):
+    """(kind, lam, n_or_low, high, p) of a market link's demand source: the numpy
+    Generator method its `demand_dist_func` calls (a string, or the method name
+    the lambda's code references, as `lambda **p: self.np_random.binomial(**p)`),
+    else the one `dist_param`'s keys name; kind 1 poisson, 2 binomial,
+    3 integers [low, high), 4 geometric (network_management.py:125-127, 257-263)."""
+    f = attrs.get("demand_dist_func")
+    names = {"poisson", "binomial", "integers", "geometric"}
+    name = f if isinstance(f, str) else None
+    if name is None and f is not None:
+        hit = names & set(getattr(getattr(f, "__code__", None), "co_names", ()))
+        name = hit.pop() if len(hit) == 1 else None
+    dp = dict(attrs.get("dist_param", {}))
+    if name is None:
+        keys = set(dp)
+        name = ("poisson" if keys <= {"lam"} else "binomial" if keys == {"n", "p"} else
+                "integers" if keys in ({"low"}, {"low", "high"}) else "geometric" if keys == {"p"} else None)
+    if name == "poisson":
+        return 1, float(dp.get("lam", 1.0)), 0, 0, 0.0
+    if name == "binomial":
+        return 2, 0.0, int(dp["n"]), 0, float(dp["p"])
+    if name == "integers":
+        lo, hi = (0, int(dp["low"])) if "high" not in dp else (int(dp["low"]), int(dp["high"]))
+        return 3, 0.0, lo, hi, 0.0
+    if name == "geometric":
+        return 4, 0.0, 0, 0, float(dp["p"])
+    raise ValueError(f"unsupported market demand source {attrs!r}")
+
+
 def net_tables(g, num_periods, user_D=None):
     """Restates network_management.py:146-195 (node/link classification and ordering)."""
     nodes = list(g.nodes())
@@ -402,8 +431,13 @@ def net_tables(g, num_periods, user_D=None):
     t["rl_node"] = np.array([mi[r] for r, _ in retail_links], np.int32)
     t["rl_p"] = np.array([g.edges[e]["p"] for e in retail_links], np.float64)
     t["rl_b"] = np.array([g.edges[e]["b"] for e in retail_links], np.float64)
-    t["rl_lam"] = np.array([g.edges[e].get("dist_param", {}).get("lam", 0.0) for e in retail_links],
-                           np.float64)
+    ms = [market_sampler(g.edges[e]) if ("dist_param" in g.edges[e] or "demand_dist_func" in g.edges[e])
+          else (1, 0.0, 0, 0, 0.0) for e in retail_links]
+    t["rl_lam"] = np.array([m[1] for m in ms], np.float64)
+    t["rl_dist"] = np.array([m[0] for m in ms] or [1], np.int32)
+    t["rl_n"] = np.array([m[2] for m in ms] or [0], np.int64)
+    t["rl_high"] = np.array([m[3] for m in ms] or [0], np.int64)
+    t["rl_dp"] = np.array([m[4] for m in ms] or [0.0], np.float64)
     uD = np.zeros((max(RL, 1), num_periods), np.float64)
     rl_user = np.zeros(max(RL, 1), np.int32)
     for e, d in (user_D or {}).items():
@@ -450,7 +484,8 @@ class OracleNet(_Base):
                                                      "is_retail", "sup", "pur", "L", "sup_is_factory",
                                                      "lp", "lg", "rl_node", "rl_p", "rl_b", "rl_lam",
                                                      "rl_user", "user_D", "succ_n", "succ_kind",
-                                                     "succ_idx", "pred_n", "pred_idx")])
+                                                     "succ_idx", "pred_n", "pred_idx", "rl_dist", "rl_n",
+                                                     "rl_high", "rl_dp")])
         self.h = lib().orc_net_create(C.byref(self.cfg), n)
         self.obs_dim = int(lib().orc_net_obs_dim(self.h))
         self.act_dim = self.topo["E"]

@@ -1177,3 +1177,52 @@ def test_net_two_wave_step_equals_one_wave(gpu, monkeypatch, graph, n):
             assert torch.equal(x, y), k
     assert torch.equal(envs[0].get_state(), envs[1].get_state())
     monkeypatch.delenv("INVSIM_NET_SPLIT")
+
+
+@pytest.mark.parametrize("dists", [("binomial", "binomial", "binomial"), ("integers", "integers", "integers"),
+                                   ("geometric", "geometric", "geometric"), ("poisson", "binomial", "integers"),
+                                   ("integers", "geometric", "poisson")])
+def test_net_market_samplers_vs_oracle(gpu, oracle, dists):
+    """Market links drawing with any numpy sampler (network_management.py:257-263):
+    the custom graph's three markets get binomial / integers / geometric /
+    Poisson demand (the generic kernel runs them; one market's integers() half
+    stays buffered in the env's bit generator for the next market's draw), two
+    episodes with the NEXT_STEP reset between them, bit-exact against the oracle
+    (whose samplers are pinned against numpy itself, test_oracle.py)."""
+    from invsim import NetInvMgmtBacklogEnv
+    from invsim.topology import custom_graph
+    params = {"binomial": {"n": 60, "p": 0.3}, "integers": {"low": 2, "high": 41}, "geometric": {"p": 0.07},
+              "poisson": {"lam": 20}}
+    g = custom_graph()
+    markets = [e for e in g.edges() if "L" not in g.edges[e]]
+    for e, fn in zip(markets, dists):
+        g.edges[e]["dist_param"] = dict(params[fn])
+        g.edges[e]["demand_dist_func"] = fn
+    n = 2000
+    env = NetInvMgmtBacklogEnv(n, device=gpu, graph=g, record_demand=True)
+    assert env.kernel_variant == (2 if set(dists) == {"poisson"} else 0)
+    orc = oracle.OracleNet(n, graph=g)
+    orc.seed(range(31, 31 + n))
+    e_obs = orc.reset()
+    obs, _ = env.reset(seed=31)
+    assert _eq_bits(obs.cpu().numpy(), e_obs)
+    rng = np.random.default_rng(4)
+    for s in range(61):
+        a = rng.uniform(0, 60, size=(n, env.action_dim)).astype(np.float32)
+        o, r, te, tr, info = env.step(torch.from_numpy(a).to(gpu))
+        if s == 30:
+            e_obs = orc.reset()
+            assert _eq_bits(o.cpu().numpy(), e_obs)
+            continue
+        e_obs, e_rew, e_tr, e_info = orc.step(a, info=True)
+        assert np.array_equal(info["demand"].cpu().numpy().reshape(e_info["D"].shape),
+                              e_info["D"].astype(np.int64)), f"demand step {s}"
+        assert _eq_bits(o.cpu().numpy(), e_obs), f"obs step {s}"
+        _assert_reward(r.cpu().numpy(), e_rew, f"step {s}")
+    # and a fused rollout continues the same streams
+    acts = rng.uniform(0, 60, size=(20, n, env.action_dim)).astype(np.float32)
+    o2, r2, _, _ = env.rollout(torch.from_numpy(acts).to(gpu))
+    for k in range(20):
+        e_obs, e_rew, _ = orc.step(acts[k])
+        assert _eq_bits(o2[k].cpu().numpy(), e_obs), f"rollout step {k}"
+        _assert_reward(r2[k].cpu().numpy(), e_rew, f"rollout step {k}")

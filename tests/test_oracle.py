@@ -248,3 +248,32 @@ def test_oracle_thread_count_independent(oracle, fam):
     oracle.set_threads(1)
     for x, y in zip(*outs):
         assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
+
+
+@pytest.mark.parametrize("fn,dp", [("binomial", {"n": 40, "p": 0.5}), ("binomial", {"n": 400, "p": 0.05}),
+                                   ("integers", {"low": 3, "high": 45}), ("integers", {"low": 25}),
+                                   ("geometric", {"p": 0.05}), ("poisson", {"lam": 7.5})])
+def test_oracle_net_market_samplers_vs_numpy(oracle, fn, dp):
+    """A market link whose demand_dist_func calls np_random.<fn>(**dist_param)
+    (network_management.py:257-263): the market draws are the only consumer of
+    the env's Generator, so D[t] of env i is numpy's own <fn> stream of seed i
+    through max(0, int(round(.)))."""
+    from invsim.topology import custom_graph
+    g = custom_graph()
+    for e in list(g.edges()):
+        if "L" not in g.edges[e]:
+            g.edges[e]["dist_param"] = dict(dp)
+            g.edges[e]["demand_dist_func"] = (lambda **p: None) if fn == "poisson" else fn
+    n, T = 16, 12
+    orc = oracle.OracleNet(n, graph=g, num_periods=T)
+    orc.seed(range(100, 100 + n))
+    orc.reset()
+    D = []
+    for _ in range(T):
+        _, _, _, info = orc.step(np.full((n, orc.act_dim), 30.0, np.float32), info=True)
+        D.append(info["D"])
+    D = np.stack(D, 1)                              # [n, T, markets]
+    for i in range(n):
+        gen = np.random.Generator(np.random.PCG64(np.random.SeedSequence(100 + i)))
+        exp = [[max(0, int(round(getattr(gen, fn)(**dp)))) for _ in range(3)] for _ in range(T)]
+        assert np.array_equal(D[i], np.array(exp, np.float64)), (fn, i)

@@ -62,14 +62,32 @@ def test_user_demand_table():
         compile_graph(default_graph(), 30, user_D={(1, 0): np.ones(5)})
 
 
-def test_non_poisson_market_rejected():
+def test_market_sampler_sources():
+    """network_management.py:257-263: the numpy method a market's demand_dist_func
+    calls (by name or from the lambda's code), else dist_param's keys."""
     import networkx as nx
-    from invsim.topology import compile_graph
+    from invsim.topology import compile_graph, market_sampler
+
+    class Env:
+        np_random = np.random.default_rng(0)
+    env = Env()
+    assert market_sampler({"dist_param": {"lam": 20}})[:2] == (1, 20.0)
+    assert market_sampler({"demand_dist_func": lambda **p: env.np_random.poisson(**p),
+                           "dist_param": {"lam": 3}})[:2] == (1, 3.0)
+    assert market_sampler({"demand_dist_func": lambda **p: env.np_random.binomial(**p),
+                           "dist_param": {"n": 5, "p": 0.5}}) == (2, 0.0, 5, 0, 0.5)
+    assert market_sampler({"dist_param": {"low": 4, "high": 9}}) == (3, 0.0, 4, 9, 0.0)
+    assert market_sampler({"demand_dist_func": "integers", "dist_param": {"low": 9}}) == (3, 0.0, 0, 9, 0.0)
+    assert market_sampler({"dist_param": {"p": 0.25}}) == (4, 0.0, 0, 0, 0.25)
+    with pytest.raises(ValueError):
+        market_sampler({"demand_dist_func": lambda **p: env.np_random.gamma(**p), "dist_param": {"shape": 2}})
+    with pytest.raises(ValueError, match="needs dist_param"):
+        market_sampler({"demand_dist_func": "binomial", "dist_param": {"n": 5}})
     g = nx.DiGraph()
     g.add_node(0)
     g.add_node(1, I0=10, h=0.1)
     g.add_node(2)
     g.add_edge(1, 0, p=1.0, b=0.1, dist_param={"n": 5, "p": 0.5})
     g.add_edge(2, 1, L=1, p=0.5, g=0.0)
-    with pytest.raises(ValueError, match="Poisson"):
-        compile_graph(g, 10)
+    t = compile_graph(g, 10).tables
+    assert t["rl_dist"].tolist() == [2] and t["rl_n"].tolist() == [5] and t["rl_dp"].tolist() == [0.5]

@@ -54,6 +54,10 @@ def main():
                 shutil.copy(roll, os.path.join(dst, f"{wl}_rollout_kernel_stats.csv"))
             subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), prof, wl, kern,
                             os.path.join(dst, f"pmc_{wl}.json")], check=True, capture_output=True)
+            if os.path.isdir(os.path.join(prof, "pmc_fetch_roll")):
+                subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), prof, wl,
+                                ROLL_KERNELS[wl], os.path.join(dst, f"pmc_{wl}_rollout.json"), "rollout"],
+                               check=True, capture_output=True)
         for mode in ("step", "rollout"):
             b = last_json(os.path.join(src, f"bench_{wl}_{mode}.log"))
             if b is None:
@@ -61,14 +65,18 @@ def main():
             with open(os.path.join(dst, f"bench_{wl}_{mode}.json"), "w") as f:
                 json.dump(b, f, indent=1)
             r = b["roofline"]
-            pmc = os.path.join(dst, f"pmc_{wl}.json")
-            pm = json.load(open(pmc)) if os.path.exists(pmc) and mode == "step" else {}
+            pmc = os.path.join(dst, f"pmc_{wl}.json" if mode == "step" else f"pmc_{wl}_rollout.json")
+            pm = json.load(open(pmc)) if os.path.exists(pmc) else {}
             rows.append(f"| {wl} | {mode} | {b['config']['envs_per_gpu']} | {b['value'] / 1e9:.3f} G | "
                         f"{r['kernel_ms_mean'] * 1e3:.2f} | {r['bytes_per_env_step']:.0f} | {r['achieved']:.0f} | "
                         f"{r['frac']:.3f} | "
                         + (f"{pm['rocprof_kernel_ns_mean'] / 1e3:.2f} | {pm['traffic_over_algorithmic']:.2f} |"
-                           if pm else
+                           if pm and pm.get('traffic_over_algorithmic') else
                            f"{(kernel_avg_ns(os.path.join(dst, f'{wl}_rollout_kernel_stats.csv'), ROLL_KERNELS[wl]) or float('nan')) / 1e3:.2f} | |"))
+    sq = os.path.join(src, "sq_newsvendor")
+    if os.path.isdir(sq):
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "sq_summary.py"), sq,
+                        os.path.join(dst, "sq_newsvendor.json")], check=True, capture_output=True)
     d = last_json(os.path.join(src, "bench_default.log"))
     if d:
         with open(os.path.join(dst, "bench_default.json"), "w") as f:

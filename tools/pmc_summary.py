@@ -1,6 +1,9 @@
 """Summarise one tools/gpu_round.sh profile directory into profiles/<round>/pmc_<workload>.json.
 
-  python tools/pmc_summary.py PROFDIR WORKLOAD KERNEL_SUBSTR OUT.json
+  python tools/pmc_summary.py PROFDIR WORKLOAD KERNEL_SUBSTR OUT.json [step|rollout]
+
+(rollout: the pmc_fetch_roll / pmc_write_roll passes and trace_roll stats of
+`bench.py --mode rollout`, K = 30 steps per launch)
 
 PROFDIR holds rocprofv3 outputs of `bench.py --workload WORKLOAD`:
 trace/run_kernel_stats.csv (--kernel-trace --stats) and separate
@@ -32,20 +35,24 @@ def counter_mean(path, name, kern):
 
 def main():
     prof, wl_name, kern, out = sys.argv[1:5]
+    mode = sys.argv[5] if len(sys.argv) > 5 else "step"
+    sfx, K = ("", 1) if mode == "step" else ("_roll", 30)
     wl = WORKLOADS[wl_name]
-    fetch, nf, meta = counter_mean(os.path.join(prof, "pmc_fetch", "run_counter_collection.csv"),
+    fetch, nf, meta = counter_mean(os.path.join(prof, "pmc_fetch" + sfx, "run_counter_collection.csv"),
                                    "FETCH_SIZE", kern)
-    write, nw, _ = counter_mean(os.path.join(prof, "pmc_write", "run_counter_collection.csv"),
+    write, nw, _ = counter_mean(os.path.join(prof, "pmc_write" + sfx, "run_counter_collection.csv"),
                                 "WRITE_SIZE", kern)
-    stats = [r for r in csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_stats.csv")))
+    stats = [r for r in csv.DictReader(open(os.path.join(prof, "trace" + sfx, "run_kernel_stats.csv")))
              if kern in r["Name"]]
     st = max(stats, key=lambda r: int(r["Calls"])) if stats else None
-    alg = (wl["B_io"] + wl["B_state"]) * wl["n"]
+    B = wl["B_io"] + wl["B_state"] if K == 1 else wl["B_io"] + wl["B_state_rollout"] / K
+    alg = B * wl["n"] * K
     hbm = 2.0 * fetch * 1024 + write * 1024 if fetch is not None and write is not None else None
     rec = {
-        "kernel": f"{st['Name'] if st else kern} ({wl['desc']}, step)",
+        "kernel": f"{st['Name'] if st else kern} ({wl['desc']}, {mode}" + (f" K={K})" if K > 1 else ")"),
         "command": f"rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE (separate passes) -- python bench.py "
-                   f"--workload {wl_name} --steps 200 --warmup 20 --no-cpu-baseline",
+                   f"--workload {wl_name}" + (" --mode rollout --steps 600 --warmup 60" if K > 1 else
+                                              " --steps 200 --warmup 20") + " --no-cpu-baseline --no-rollout-line",
         "calibration": "tools/pmc_calib.hip on MI355X: FETCH_SIZE = 0.500 x bytes for 8-B and 16-B/lane "
                        "streaming reads -> x2; WRITE_SIZE = 1.000 x bytes",
         "FETCH_SIZE_KiB_mean": fetch, "FETCH_SIZE_dispatches": nf,
