@@ -41,15 +41,15 @@ sys.path.insert(0, os.path.join(ROOT, "or-gym-inventory_amd"))
 # B_io + state/K for a fused K-step rollout
 WORKLOADS = {
     "invmgmt_backlog": dict(cls="InvManagementBacklogEnv", n=65536, B_io=298, B_state=448,
-                            B_state_rollout=880, dtype="int64",
+                            B_state_rollout=880, dtype="int64", agent=("BaseStockAgent", 1.0), B_act=24,
                             desc="InvManagementBacklogEnv 4-echelon default, 65536 instances"),
     "invmgmt_lostsales": dict(cls="InvManagementLostSalesEnv", n=32768, B_io=298, B_state=384,
-                              B_state_rollout=816, dtype="int64",
+                              B_state_rollout=816, dtype="int64", agent=("BaseStockAgent", 1.0), B_act=24,
                               desc="InvManagementLostSalesEnv 4-echelon, 32768 instances per GPU"),
     "newsvendor": dict(cls="NewsvendorEnv", n=65536, B_io=54, B_state=136, B_state_rollout=136,
-                       dtype="f32/f64", desc="NewsvendorEnv default, 65536 instances, Poisson demand"),
+                       dtype="f32/f64", agent=("OrderUpToHeuristicAgent", 1.0), B_act=4, desc="NewsvendorEnv default, 65536 instances, Poisson demand"),
     "net_backlog": dict(cls="NetInvMgmtBacklogEnv", n=32768, B_io=326, B_state=720,
-                        B_state_rollout=1136, dtype="f64",
+                        B_state_rollout=1136, dtype="f64", agent=("ConstantOrderAgent", 0.1), B_act=44,
                         desc="NetInvMgmtBacklogEnv default topology, 32768 instances"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -61,12 +61,18 @@ def parse():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workload", default="invmgmt_backlog", choices=sorted(WORKLOADS))
-    ap.add_argument("--mode", default="step", choices=["step", "rollout"])
+    ap.add_argument("--mode", default="step", choices=["step", "rollout", "policy"],
+                    help="policy: K-step rollouts with the workload's heuristic agent in the kernel "
+                         "(invsim_rollout_policy; BaseStock / OrderUpTo / ConstantOrder)")
     ap.add_argument("--rollout-k", type=int, default=30)
     ap.add_argument("--n-envs", type=int, default=0)
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: the workload's env count is the GLOBAL batch, split over ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fold", default="inline", choices=["side", "inline", "none"],
+                    help="episodic-return fold of the timed outputs: between blocks on the kernel stream "
+                         "(default), on a side stream (measured slower: it shares the CUs with the step "
+                         "kernels), or off (A/B only: no episode_stats)")
     ap.add_argument("--no-rollout-line", action="store_true",
                     help="step mode: skip the K-step rollout region reported under 'rollout'")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
@@ -192,11 +198,15 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     N, O = env.num_envs, env.obs_dim
-    K = args.rollout_k if mode == "rollout" else 0
+    K = args.rollout_k if mode in ("rollout", "policy") else 0
     pool = max(1, args.pool if mode == "step" else 2)
-    acts = make_actions(env, pool, K, gen)
+    acts = make_actions(env, pool, K, gen) if mode != "policy" else []
     ptrs = [a.data_ptr() for a in acts]
-    R = K if K else 32                              # slab rows = steps per fold
+    # slab rows = steps per fold: 128 single steps, or 4 launches of K steps.  The
+    # fold is a separate launch between blocks (~9 us of stream time each,
+    # measured), so blocks are long
+    LPB = 4                                         # launches per block (rollout / policy)
+    R = LPB * K if K else 128
     # two output slabs: the fold of one runs on a side stream while the steps
     # write the other (events order slab reuse), so the reduction overlaps the
     # env kernels instead of sitting between them
@@ -223,13 +233,32 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
             if rc:
                 raise RuntimeError(invsim._capi.last_error(h))
         steps_per_call = 1
-    else:
+    elif mode == "rollout":
         fn = lib.invsim_rollout
-        calls_per_block = 1
+        calls_per_block = LPB
 
         def one(i, row, sl):
             pr, pt, pu = slab_ptrs[sl]
-            rc = fn(h, K, ptrs[i % pool], po, pr, pt, pu, sp)
+            rc = fn(h, K, ptrs[i % pool], po, pr + 8 * row * N, pt + row * N, pu + row * N, sp)
+            if rc:
+                raise RuntimeError(invsim._capi.last_error(h))
+        steps_per_call = K
+    else:
+        # the workload's heuristic agent inside the kernel: no action input,
+        # the evaluate_agent sums accumulated per env (invsim_rollout_policy)
+        import ctypes
+        cls_name, arg = wl["agent"]
+        spec, keep = getattr(invsim.policies, cls_name)(arg).device_spec(env)
+        md = ctypes.c_int32()
+        lib.invsim_metrics_dim(h, ctypes.byref(md))
+        metrics = torch.zeros((N, md.value), dtype=torch.float64, device=dev)
+        fn = lib.invsim_rollout_policy
+        calls_per_block = LPB
+
+        def one(i, row, sl):
+            pr, pt, pu = slab_ptrs[sl]
+            rc = fn(h, K, ctypes.byref(spec), po, pr + 8 * row * N, pt + row * N, pu + row * N, None,
+                    metrics.data_ptr(), sp)
             if rc:
                 raise RuntimeError(invsim._capi.last_error(h))
         steps_per_call = K
@@ -256,14 +285,17 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
             if timed:
                 evs[bi // calls_per_block][0].record(stream)
             for j in range(nb):
-                one(bi + j, j * (rows_per_call if K == 0 else 0), sl)
+                one(bi + j, j * rows_per_call, sl)
             if timed:
                 evs[bi // calls_per_block][1].record(stream)
-            ev_out[sl].record(stream)
-            fstream.wait_event(ev_out[sl])
-            rows = nb * rows_per_call if K == 0 else K
-            _fold_rows(stats, rew[sl], term[sl], trunc[sl], rows, fsp)
-            ev_free[sl].record(fstream)
+            rows = nb * rows_per_call
+            if args.fold == "side":
+                ev_out[sl].record(stream)
+                fstream.wait_event(ev_out[sl])
+                _fold_rows(stats, rew[sl], term[sl], trunc[sl], rows, fsp)
+                ev_free[sl].record(fstream)
+            elif args.fold == "inline":
+                _fold_rows(stats, rew[sl], term[sl], trunc[sl], rows, sp)
             blk[0] += 1
 
     region(warm, False)
@@ -290,6 +322,8 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     # the fast stream reads an 8-B key instead of the 32-B PCG64 state and writes no state back
     dB = -40 if env.demand_stream == "philox" else 0
     B = wl["B_io"] + ((wl["B_state_rollout"] + dB) / K if K else wl["B_state"] + dB)
+    if mode == "policy":   # no action input; the per-env metric sums read and written once per launch
+        B += -wl["B_act"] + 16 * metrics.shape[1] / K
     achieved = B * N * steps_per_call / (kern_ms * 1e-3) / 1e9
     achieved_wall = B * N * total_steps / el / 1e9
     return dict(el=el, calls=calls, warm=warm, steps_per_call=steps_per_call, total_steps=total_steps,
@@ -315,7 +349,7 @@ def _pmc(workload, mode, n_match):
     """The newest round's PMC summary for this workload and mode
     (profiles/rNN/pmc_<workload>[_rollout].json, tools/pmc_summary.py)."""
     import glob
-    suffix = "" if mode == "step" else "_rollout"
+    suffix = {"step": "", "rollout": "_rollout", "policy": "_policy"}[mode]
     pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", f"pmc_{workload}{suffix}.json")))
     if not pmcs or not n_match:
         return None, None
@@ -383,7 +417,9 @@ def main():
         "dtype": wl["dtype"],
         "data": "synthetic (pre-generated random actions in HBM, seeds 0..N-1 per global env index)",
         "config": {"workload": wl["desc"], "envs_per_gpu": N, "global_envs": N * world,
-                   "mode": args.mode + (f" K={r['K']}" if r["K"] else ""), "autoreset": "next_step",
+                   "mode": args.mode + (f" K={r['K']}" if r["K"] else "") +
+                           (f" agent={wl['agent'][0]}({wl['agent'][1]})" if args.mode == "policy" else ""),
+                   "autoreset": "next_step",
                    "parallelism": f"dp{world} (env sharding, no data-path collective)",
                    "backend": (backend if world > 1 else None), "demand_stream": args.demand_stream},
         "roofline": _roofline(r, traffic, traffic_src),

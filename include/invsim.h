@@ -299,8 +299,9 @@ int invsim_set_info_demand(invsim_handle *h, int64_t *demand);
  *   Newsvendor f64 [N][5]:          revenue, purchase_cost, holding_cost,
  *                                    lost_sales_penalty (newsvendor.py:149-170, 195-199)
  *                                    and their NumPy-2 kinds packed as
- *                                    k_rev + 3 k_pur + 9 k_hold + 27 k_pen
- *                                    (0 Python float, 1 np.float32, 2 np.float64) */
+ *                                    k_rev + 4 k_pur + 16 k_hold + 64 k_pen
+ *                                    (0 Python float, 1 np.float32, 2 np.float64,
+ *                                    3 Python int) */
 int invsim_info_record_dim(const invsim_handle *h, int32_t *dim);
 int invsim_set_info_record(invsim_handle *h, void *record);
 

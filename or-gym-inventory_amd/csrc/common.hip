@@ -67,8 +67,10 @@ episode_fold_kernel(const double *rew, const uint8_t *term, const uint8_t *trunc
 #pragma unroll
             for (int u = 0; u < FB; ++u) {
                 const int64_t i = (int64_t)min(k0 + u, K - 1) * N + e;
-                x[u] = rew[i];
-                d[u] = (uint8_t)((term ? term[i] : 0) | (trunc ? trunc[i] : 0));
+                // streamed once: non-temporal, so the env state stays cached for the next step launch
+                x[u] = __builtin_nontemporal_load(rew + i);
+                d[u] = (uint8_t)((term ? __builtin_nontemporal_load(term + i) : 0) |
+                                 (trunc ? __builtin_nontemporal_load(trunc + i) : 0));
             }
 #pragma unroll
             for (int u = 0; u < FB; ++u) {

@@ -20,7 +20,9 @@ namespace {
 __device__ uint64_t g_tbuf[TB_WAVES * TB_PROBES];
 #endif
 
-enum { K_PY = 0, K_F32 = 1, K_F64 = 2 };
+// NumPy-2 scalar kinds: Python float, np.float32, np.float64, Python int (poisson()
+// draws and the int operands of max(1, .) / max(0, .), newsvendor.py:105-106,143-153)
+enum { K_PY = 0, K_F32 = 1, K_F64 = 2, K_INT = 3 };
 struct Tv {
     double v;
     int k;
@@ -41,7 +43,8 @@ __device__ __forceinline__ Tv tv_bin(Tv a, Tv b) {
     if (OP == '+') r = a.v + b.v;
     else if (OP == '-') r = a.v - b.v;
     else r = a.v * b.v;
-    return Tv{r, (a.k == K_F64 || b.k == K_F64) ? K_F64 : K_PY};
+    // Python int op Python int stays int (exact here: small integers); any float makes a float
+    return Tv{r, (a.k == K_F64 || b.k == K_F64) ? K_F64 : (a.k == K_INT && b.k == K_INT) ? K_INT : K_PY};
 }
 
 // numpy clip of a float64: NaN propagates, a bound is taken only when strictly
@@ -328,21 +331,23 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
     if (dpre < 0) s.g.sub(0);
     const int64_t d = dpre >= 0 ? dpre : env_poisson_dyn(s.g, s.par[4], lg_l, RHS_LDS_MAX);
     TPROBE(2);
-    const Tv ZERO = tv(0.0, K_PY);
+    const Tv ZERO = tv(0.0, K_INT);                                         // the 0 of max(0, .)
     const Tv oq = tv(np_clip((double)action, 0.0, P.max_order), K_F64);    // :131-132
     const float S5 = np_sum<float>(L, pos);                                 // :135
     const Tv inv = (L > 0) ? tv((double)pos(0), K_F32) : oq;                // :136-141
     const Tv cap = tv_bin<'-'>(tv(P.max_inventory, K_PY), tv((double)S5, K_F32));
     const Tv m1 = (cap.v < oq.v) ? cap : oq;                                // min(oq, cap)
     const Tv q = (m1.v > 0) ? m1 : ZERO;                                    // :143
-    const Tv dv = tv((double)d, K_PY);
+    const Tv dv = tv((double)d, K_INT);                                     // poisson() -> Python int
     const Tv sales = (dv.v < inv.v) ? dv : inv;                             // :149
-    const Tv revenue = tv_bin<'*'>(sales, tv(s.par[0], K_PY));              // :150
+    // price / cost are the Python int 1 when max(1, .) took its first operand (:105-106)
+    const Tv price = tv(s.par[0], s.par[0] == 1.0 ? K_INT : K_PY), cost = tv(s.par[1], s.par[1] == 1.0 ? K_INT : K_PY);
+    const Tv revenue = tv_bin<'*'>(sales, price);                           // :150
     const Tv ex = tv_bin<'-'>(inv, dv);
     const Tv excess = (ex.v > 0) ? ex : ZERO;                               // :152
     const Tv sh = tv_bin<'-'>(dv, inv);
     const Tv shortage = (sh.v > 0) ? sh : ZERO;                             // :153
-    const Tv purchase = tv_bin<'*'>(q, tv(s.par[1], K_PY));                 // :162
+    const Tv purchase = tv_bin<'*'>(q, cost);                               // :162
     const Tv holding = tv_bin<'*'>(excess, tv(s.par[2], K_PY));             // :166
     const Tv penalty = tv_bin<'*'>(shortage, tv(s.par[3], K_PY));           // :167
     const Tv r = tv_bin<'-'>(tv_bin<'-'>(tv_bin<'-'>(revenue, purchase), holding), penalty); // :170
@@ -366,7 +371,7 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
         rr[1] = purchase.v;
         rr[2] = holding.v;
         rr[3] = penalty.v;
-        rr[4] = (double)(revenue.k + 3 * purchase.k + 9 * holding.k + 27 * penalty.k);
+        rr[4] = (double)(revenue.k + 4 * purchase.k + 16 * holding.k + 64 * penalty.k);
     }
     TPROBE(3);
     return sc + 1 >= P.step_limit;                                          // :190

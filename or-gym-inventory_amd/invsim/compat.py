@@ -168,6 +168,9 @@ class NewsvendorView(_View):
     def _info(self):
         p = self._v.params()[0].cpu().numpy()
         self.price, self.cost, self.h, self.k, self.mu = (float(x) for x in p)
+        # max(1, .) keeps its Python int operand (newsvendor.py:105-106)
+        self.price = 1 if self.price == 1.0 else self.price
+        self.cost = 1 if self.cost == 1.0 else self.cost
         return {"price": self.price, "cost": self.cost, "holding_cost_rate": self.h, "penalty_cost_rate": self.k,
                 "demand_mean": self.mu, "lead_time": self._v.lead_time, "step_count": self.step_count}
 
@@ -177,7 +180,7 @@ class NewsvendorView(_View):
         self.period = self.step_count
         out = self._info()
         out["demand"] = int(info["demand"][0])
-        typ = (float, np.float32, np.float64)
+        typ = (float, np.float32, np.float64, int)
         for k in ("revenue", "purchase_cost", "holding_cost", "lost_sales_penalty"):   # newsvendor.py:195-199
             out[k] = typ[int(info[k + "_kind"][0])](info[k][0].item())
         return obs[0].cpu().numpy(), float(r[0]), bool(te[0]), bool(tr[0]), out

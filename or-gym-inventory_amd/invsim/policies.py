@@ -217,12 +217,13 @@ def evaluate_agent(agent, env_cls, env_config=None, n_episodes=100, seed_offset=
         dt = time.perf_counter() - t0
         met = met[:n_loc]
         family = env.family
+        env_dev = env.device
     finally:
         env.close()
     if world > 1:
         met = _gather_rows(met, n_episodes, world, rank, group)
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
-            else torch.device("cpu")
+        # both collectives on the env's device (RCCL), or on the host (gloo)
+        dev = env_dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         dt = float(t.item())

@@ -50,7 +50,9 @@ class InvSimVecEnv(_SB3VecEnv):
         self._seed = None
         self._seeds = [None for _ in range(self.num_envs)]
         self._options = [{} for _ in range(self.num_envs)]
-        self.reset_infos = [dict(info) for _ in range(self.num_envs)]
+        # SB3 2.x: one info dict per env, holding that env's own entries
+        self.reset_infos = [{k: (v[i].cpu().numpy() if torch.is_tensor(v) else v) for k, v in info.items()}
+                            for i in range(self.num_envs)]
         self._obs = obs
         return obs.cpu().numpy()
 

@@ -123,11 +123,11 @@ class InvSimVectorEnv:
             for i, k in enumerate(("period_profit", "revenue", "procurement_cost", "holding_cost", "penalty_cost")):
                 info[k] = f[:, i]
         elif self.family == _capi.INVSIM_NEWSVENDOR:
-            # newsvendor.py:195-199; kinds: 0 Python float, 1 np.float32, 2 np.float64
+            # newsvendor.py:195-199; kinds: 0 Python float, 1 np.float32, 2 np.float64, 3 Python int
             kinds = rec[:, 4].to(torch.int64)
             for i, k in enumerate(("revenue", "purchase_cost", "holding_cost", "lost_sales_penalty")):
                 info[k] = rec[:, i]
-                info[k + "_kind"] = (kinds // (3 ** i)) % 3
+                info[k + "_kind"] = (kinds // (4 ** i)) % 4
         else:
             RL, J, E = len(self.retail_links), len(self.main_nodes), len(self.reorder_links)
             o = 0

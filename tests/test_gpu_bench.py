@@ -110,3 +110,15 @@ def test_bench_gpus_flag_strong_net():
     _check_line(d, 2, 20, 5)
     assert d["scaling"] == "strong" and d["ranks"] == 2
     assert d["config"]["envs_per_gpu"] == 16384 and d["config"]["global_envs"] == 32768
+
+
+@pytest.mark.parametrize("wl", ["invmgmt_backlog", "newsvendor", "net_backlog"])
+def test_bench_policy_mode(wl):
+    """--mode policy: K-step rollouts with the workload's heuristic agent in the kernel"""
+    p = subprocess.run([sys.executable, "bench.py", "--workload", wl, "--mode", "policy", "--steps", "60",
+                        "--warmup", "30", "--no-cpu-baseline", "--no-rollout-line"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _last_json(p.stdout)
+    assert d["value"] > 0 and d["steps"] == 60 and "agent=" in d["config"]["mode"]
+    assert d["episode_stats"]["reward_sum"] != 0

@@ -14,7 +14,7 @@ from conftest import NV_GOLDENS, load_golden, nv_kwargs
 
 pytestmark = pytest.mark.gpu
 
-KINDS = (float, np.float32, np.float64)
+KINDS = (float, np.float32, np.float64, int)
 
 
 def ref_components(prev_obs, action, demand, params, cfg):
@@ -23,6 +23,8 @@ def ref_components(prev_obs, action, demand, params, cfg):
     max_q = cfg.get("max_order_quantity", 2000)
     max_inv = cfg.get("max_inventory", 4000)
     price, cost, h, k = (float(x) for x in params[:4])
+    price = 1 if price == 1.0 else price                              # max(1, .) -> the Python int 1 (:105-106)
+    cost = 1 if cost == 1.0 else cost
     state = np.asarray(prev_obs, np.float32)
     order_qty = np.clip(float(action), 0, max_q)                        # :130-131
     cur = state[5:].sum()                                              # :134
@@ -40,7 +42,7 @@ def ref_components(prev_obs, action, demand, params, cfg):
 
 
 def _kind(x):
-    return 1 if isinstance(x, np.float32) else 2 if isinstance(x, np.float64) else 0
+    return 1 if isinstance(x, np.float32) else 2 if isinstance(x, np.float64) else 3 if type(x) is int else 0
 
 
 @pytest.mark.parametrize("name", NV_GOLDENS)
@@ -73,11 +75,13 @@ def test_newsvendor_step_info_costs_vs_reference_expressions(gpu, name):
     assert ("revenue", 1) in seen or ("revenue", 0) in seen
 
 
-def test_newsvendor_compat_view_info_types(gpu):
+@pytest.mark.parametrize("p_max", [100.0, 0.5])
+def test_newsvendor_compat_view_info_types(gpu, p_max):
     """The single-env view's info carries the components with the reference's
-    scalar types."""
+    scalar types (p_max = 0.5: price and cost are the Python int 1 of max(1, .),
+    so revenue and a zero order's purchase cost are Python ints)."""
     from invsim import compat
-    env = compat.make("NewsvendorEnv", device=gpu, lead_time=2, step_limit=6)
+    env = compat.make("NewsvendorEnv", device=gpu, lead_time=2, step_limit=6, p_max=p_max)
     obs, info = env.reset(seed=3)
     prev = obs.copy()
     for a in (50.0, 0.0, 3000.0, 7.5, 0.0):
@@ -89,3 +93,5 @@ def test_newsvendor_compat_view_info_types(gpu):
             assert np.float64(info[k]) == np.float64(x)
         assert r == float(((exp[0] - exp[1]) - exp[2]) - exp[3])
         prev = obs.copy()
+    if p_max < 1:
+        assert type(info["price"]) is int and type(info["cost"]) is int

@@ -1219,10 +1219,11 @@ def test_net_market_samplers_vs_oracle(gpu, oracle, dists):
                               e_info["D"].astype(np.int64)), f"demand step {s}"
         assert _eq_bits(o.cpu().numpy(), e_obs), f"obs step {s}"
         _assert_reward(r.cpu().numpy(), e_rew, f"step {s}")
-    # and a fused rollout continues the same streams
+    # and a fused rollout continues the same streams (its first step is the NEXT_STEP reset)
     acts = rng.uniform(0, 60, size=(20, n, env.action_dim)).astype(np.float32)
     o2, r2, _, _ = env.rollout(torch.from_numpy(acts).to(gpu))
-    for k in range(20):
+    assert _eq_bits(o2[0].cpu().numpy(), orc.reset())
+    for k in range(1, 20):
         e_obs, e_rew, _ = orc.step(acts[k])
         assert _eq_bits(o2[k].cpu().numpy(), e_obs), f"rollout step {k}"
         _assert_reward(r2[k].cpu().numpy(), e_rew, f"rollout step {k}")

@@ -13,6 +13,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROLL_KERNELS = {"invmgmt_backlog": "im_roll3_kernel", "invmgmt_lostsales": "im_roll3o_kernel",
                 "newsvendor": "nv_roll_kernel", "net_backlog": "net_roll3o_kernel"}
+POL_KERNELS = {"invmgmt_backlog": "im_run_kernel", "invmgmt_lostsales": "im_run_kernel",
+               "newsvendor": "nv_run_kernel", "net_backlog": "net_spec_kernel"}
 KERNELS = {"invmgmt_backlog": "im_split_kernel", "invmgmt_lostsales": "im_split_kernel",
            "newsvendor": "nv_step1_kernel", "net_backlog": "net_step2_kernel"}
 
@@ -58,14 +60,20 @@ def main():
                 subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), prof, wl,
                                 ROLL_KERNELS[wl], os.path.join(dst, f"pmc_{wl}_rollout.json"), "rollout"],
                                check=True, capture_output=True)
-        for mode in ("step", "rollout"):
+            if os.path.isdir(os.path.join(prof, "pmc_fetch_pol")):
+                shutil.copy(os.path.join(prof, "trace_pol", "run_kernel_stats.csv"),
+                            os.path.join(dst, f"{wl}_policy_kernel_stats.csv"))
+                subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), prof, wl,
+                                POL_KERNELS[wl], os.path.join(dst, f"pmc_{wl}_policy.json"), "policy"],
+                               check=True, capture_output=True)
+        for mode in ("step", "rollout", "policy"):
             b = last_json(os.path.join(src, f"bench_{wl}_{mode}.log"))
             if b is None:
                 continue
             with open(os.path.join(dst, f"bench_{wl}_{mode}.json"), "w") as f:
                 json.dump(b, f, indent=1)
             r = b["roofline"]
-            pmc = os.path.join(dst, f"pmc_{wl}.json" if mode == "step" else f"pmc_{wl}_rollout.json")
+            pmc = os.path.join(dst, f"pmc_{wl}.json" if mode == "step" else f"pmc_{wl}_{mode}.json")
             pm = json.load(open(pmc)) if os.path.exists(pmc) else {}
             rows.append(f"| {wl} | {mode} | {b['config']['envs_per_gpu']} | {b['value'] / 1e9:.3f} G | "
                         f"{r['kernel_ms_mean'] * 1e3:.2f} | {r['bytes_per_env_step']:.0f} | {r['achieved']:.0f} | "

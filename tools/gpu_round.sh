@@ -32,6 +32,8 @@ for part in $PARTS; do
       run timeout -k 10 120 python bench.py --workload $w $B > $OUT/bench_${w}_step.log 2>&1
       run timeout -k 10 120 python bench.py --workload $w --mode rollout --steps 1200 $B \
           > $OUT/bench_${w}_rollout.log 2>&1
+      run timeout -k 10 120 python bench.py --workload $w --mode policy --steps 1200 $B \
+          > $OUT/bench_${w}_policy.log 2>&1
       tail -n1 $OUT/bench_${w}_step.log | cut -c1-200
     done ;;
   prof)
@@ -49,6 +51,12 @@ for part in $PARTS; do
           python bench.py --workload $w --mode rollout --steps 600 --warmup 60 $B > $P.fetch_roll.log 2>&1
       run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/pmc_write_roll -o run -- \
           python bench.py --workload $w --mode rollout --steps 600 --warmup 60 $B > $P.write_roll.log 2>&1
+      run timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace_pol -o run -- \
+          python bench.py --workload $w --mode policy --steps 600 --warmup 60 $B > $P.trace_pol.log 2>&1
+      run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/pmc_fetch_pol -o run -- \
+          python bench.py --workload $w --mode policy --steps 600 --warmup 60 $B > $P.fetch_pol.log 2>&1
+      run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/pmc_write_pol -o run -- \
+          python bench.py --workload $w --mode policy --steps 600 --warmup 60 $B > $P.write_pol.log 2>&1
     done ;;
   sq)
     # Newsvendor step (nv_step1_kernel) and rollout (nv_roll_kernel): issue vs wait

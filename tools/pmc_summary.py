@@ -36,7 +36,7 @@ def counter_mean(path, name, kern):
 def main():
     prof, wl_name, kern, out = sys.argv[1:5]
     mode = sys.argv[5] if len(sys.argv) > 5 else "step"
-    sfx, K = ("", 1) if mode == "step" else ("_roll", 30)
+    sfx, K = {"step": ("", 1), "rollout": ("_roll", 30), "policy": ("_pol", 30)}[mode]
     wl = WORKLOADS[wl_name]
     fetch, nf, meta = counter_mean(os.path.join(prof, "pmc_fetch" + sfx, "run_counter_collection.csv"),
                                    "FETCH_SIZE", kern)
@@ -46,12 +46,15 @@ def main():
              if kern in r["Name"]]
     st = max(stats, key=lambda r: int(r["Calls"])) if stats else None
     B = wl["B_io"] + wl["B_state"] if K == 1 else wl["B_io"] + wl["B_state_rollout"] / K
+    if mode == "policy":   # as bench.py: no action input, per-env metric sums once per launch
+        md = {"invmgmt_backlog": 6, "invmgmt_lostsales": 6, "newsvendor": 2, "net_backlog": 11}[wl_name]
+        B += -wl["B_act"] + 16 * md / K
     alg = B * wl["n"] * K
     hbm = 2.0 * fetch * 1024 + write * 1024 if fetch is not None and write is not None else None
     rec = {
         "kernel": f"{st['Name'] if st else kern} ({wl['desc']}, {mode}" + (f" K={K})" if K > 1 else ")"),
         "command": f"rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE (separate passes) -- python bench.py "
-                   f"--workload {wl_name}" + (" --mode rollout --steps 600 --warmup 60" if K > 1 else
+                   f"--workload {wl_name}" + (f" --mode {mode} --steps 600 --warmup 60" if K > 1 else
                                               " --steps 200 --warmup 20") + " --no-cpu-baseline --no-rollout-line",
         "calibration": "tools/pmc_calib.hip on MI355X: FETCH_SIZE = 0.500 x bytes for 8-B and 16-B/lane "
                        "streaming reads -> x2; WRITE_SIZE = 1.000 x bytes",
