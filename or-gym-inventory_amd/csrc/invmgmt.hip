@@ -939,9 +939,16 @@ struct ImLt3 {
     }
 };
 
-template <int L0, int L1, int L2, bool BACKLOG>
+// POL (invsim_rollout_policy with BASE_STOCK or CONSTANT): the dynamics wave
+// computes each step's order from its registers instead of loading it --
+// BaseStockAgent.get_action (benchmark_InvManagementBacklogEnv.py:152-198) needs
+// I[t] and the requested orders of the last L_i periods, ages 1 .. L_i of the
+// window it already holds (plus the age-D row, wold) -- every output is
+// optional, and the evaluate_agent sums accumulate in registers (as
+// im_launch_step / im_step_regs, same order).
+template <int L0, int L1, int L2, bool BACKLOG, bool POL>
 __global__ void __launch_bounds__(2 * WAVE)
-im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
+im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     using G = ImLt3<L0, L1, L2>;
     constexpr int M1 = G::M1, D = G::D, O = G::O, CH = G::CH;
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
@@ -1006,7 +1013,18 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
     }
     int64_t nact[M1];
 #pragma unroll
-    for (int i = 0; i < M1; i++) nact[i] = io.act[el * M1 + i];
+    for (int i = 0; i < M1; i++) nact[i] = POL ? 0 : io.act[el * M1 + i];
+    // POL: the age-D requested-order row (slot t mod D, before step t overwrites it)
+    int64_t wold[M1];
+#pragma unroll
+    for (int i = 0; i < M1; i++) {
+        wold[i] = 0;
+        if (POL && G::lt(i) == D) wold[i] = alog_get(P, ((int64_t)((uint32_t)t % (uint32_t)D) * S + el) * M1 + i);
+    }
+    constexpr int MD = 6;                                 // metrics (invsim.h INVSIM_METRICS_*)
+    double met[MD];
+#pragma unroll
+    for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
     double napow = P.alpha_pow[t < P.periods ? t : 0];   // alpha**t of the next step, prefetched
     int64_t dlast = 0;
     bool last_real = false;
@@ -1024,7 +1042,7 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 const int tn = (t >= P.periods) ? 0 : t + 1;     // the next launch step's period
                 napow = P.alpha_pow[tn < P.periods ? tn : 0];
             }
-            if (k + 1 < K) {                       // prefetch the next step's actions
+            if (!POL && k + 1 < K) {               // prefetch the next step's actions
 #pragma unroll
                 for (int i = 0; i < M1; i++) nact[i] = io.act[((int64_t)(k + 1) * N + el) * M1 + i];
             }
@@ -1035,7 +1053,7 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 for (int q = 0; q <= M1; q++) B[q] = 0;
 #pragma unroll
                 for (int q = 0; q < O; q++) trow[q] = (q < M1) ? P.I0[q] : 0;
-                if (valid) {
+                if (valid && (!POL || io.rew)) {
                     out_store(io.rew + oi, 0.0);
                     out_store(io.term + oi, (uint8_t)0);
                     out_store(io.trunc + oi, (uint8_t)0);
@@ -1043,6 +1061,35 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 t = 0;
             } else {
                 const int64_t d = db[kk * WAVE + lane];
+                if (POL) {
+                    if (pol.kind == POL_BASE_STOCK) {   // im_base_stock from the register windows
+#pragma unroll
+                        for (int i = 0; i < M1; i++) {
+                            constexpr int DD = D;
+                            int64_t pos = I[i];                                 // observation[:M1] = I[t]
+                            int64_t pipe = 0;
+#pragma unroll
+                            for (int a = 1; a <= G::lt(i); a++) {               // action_log[max(0, t - L_i) : t, i]
+                                const int64_t v = (a <= DD - 1) ? wv[(DD - 1 - a) >= 0 ? DD - 1 - a : 0][i] : wold[i];
+                                if (t - a >= 0) pipe = wrap_add(pipe, v);
+                            }
+                            if (G::lt(i) > 0) pos = wrap_add(pos, pipe);
+                            const double target = ((double)(G::lt(i) + 1) * pol.mu) * pol.sf;
+                            double x = target - (double)pos;
+                            x = (x > 0) ? x : 0.0;                              // np.maximum(0, .)
+                            x = (x < 0.0) ? 0.0 : x;                            // np.clip(., 0, c)
+                            x = (x > (double)P.c[i]) ? (double)P.c[i] : x;
+                            req[i] = (int64_t)x;
+                        }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < M1; i++) req[i] = pol.ci[i];
+                    }
+                    if (valid && pol.act_out) {
+#pragma unroll
+                        for (int i = 0; i < M1; i++) out_store((int64_t *)pol.act_out + oi * M1 + i, req[i]);
+                    }
+                }
                 int64_t ordreq[M1], R[M1], Icur[M1];
 #pragma unroll
                 for (int i = 0; i < M1; i++) req[i] = req[i] > 0 ? req[i] : 0;   // :250
@@ -1081,6 +1128,17 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 }
                 const double profit = np_sum<double>(M1 + 1, [&](int q) { return term[q]; });
                 const double reward = apow * profit;                            // :322
+                if (POL) {   // evaluate_agent metrics (benchmark_InvManagementBacklogEnv.py:378-399)
+                    met[2] += (double)d;                                        // demand_realized
+                    met[3] += (double)Sv[0];                                    // sales[0]
+                    met[4] += (double)U[0];                                     // unfulfilled[0]
+                    int64_t es = 0;                                             // sum(max(0, ending_inventory))
+#pragma unroll
+                    for (int i = 0; i < M1; i++) es = wrap_add(es, Icur[i] > 0 ? Icur[i] : 0);
+                    met[5] += (double)es;
+                    met[0] += reward;                                           // episode_reward += reward
+                    met[1] += 1.0;                                              // episode_steps
+                }
                 // observation (:354-391): I, then the window rows t+1-n .. t, zeros after
                 const int n = (t + 1 < D) ? t + 1 : D;
 #pragma unroll
@@ -1110,9 +1168,11 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                         st_store(P.alog32 + wb + i, wide ? IM_WIDE : (uint32_t)req[i]);
                         if (wide) st_store(P.alog + wb + i, req[i]);
                     }
-                    out_store(io.rew + oi, reward);
-                    out_store(io.term + oi, (uint8_t)0);
-                    out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.periods ? 1 : 0));   // :350
+                    if (!POL || io.rew) {
+                        out_store(io.rew + oi, reward);
+                        out_store(io.term + oi, (uint8_t)0);
+                        out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.periods ? 1 : 0));   // :350
+                    }
                 }
                 // age the windows by one period
 #pragma unroll
@@ -1123,6 +1183,10 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                         for (int a = 0; a + 1 < G::W(i); a++) rw[i][a] = rw[i][a + 1];
                         rw[i][G::W(i) - 1] = R[i];
                     }
+                }
+                if (POL && D > 1) {
+#pragma unroll
+                    for (int i = 0; i < M1; i++) wold[i] = wv[0][i];             // age D - 1 -> age D
                 }
 #pragma unroll
                 for (int a = 0; a + 2 < D; a++) {
@@ -1143,8 +1207,9 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
             }
             wave_lds_sync();
 #ifndef INVSIM_ABL_ROLL_NO_STORE
-            store_tile<(O * WAVE * 8 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + ((int64_t)k * N + e0) * O,
-                                                                    (int64_t)nvalid * O, lane);
+            if (!POL || io.obs)
+                store_tile<(O * WAVE * 8 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + ((int64_t)k * N + e0) * O,
+                                                                        (int64_t)nvalid * O, lane);
 #endif
             wave_lds_sync();
         }
@@ -1158,6 +1223,10 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
             for (int q = 0; q <= M1; q++) st_store(P.B + q * S + e, B[q]);
         }
         if (P.cm.info_demand && last_real) P.cm.info_demand[e] = dlast;
+        if (POL && pol.metrics) {
+#pragma unroll
+            for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
+        }
     }
 }
 
@@ -1498,6 +1567,12 @@ inline bool im_roll_enabled() {
     return !(s && s[0] == '0');
 }
 
+// INVSIM_IM_POL_ROLL=0 keeps policy rollouts on im_run_kernel (A/B, tests)
+inline bool im_pol_roll_enabled() {
+    const char *s = getenv("INVSIM_IM_POL_ROLL");
+    return !(s && s[0] == '0');
+}
+
 // INVSIM_IM_AHEAD=0 turns the demand lookahead off (A/B measurements)
 inline bool im_ahead_enabled() {
     const char *s = getenv("INVSIM_IM_AHEAD");
@@ -1621,11 +1696,19 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     }
     // lock-step rollout of the reference's default lead times: register windows
     // and a demand wave (im_roll3_kernel)
-    if (!pol && io.K > 1 && t_u >= 0 && p.cm.autoreset != AR_SAME_STEP && p.dist == 1 && !p.cm.info_rec &&
-        M1 == 3 && p.L[0] == 1 && p.L[1] == 5 && p.L[2] == 10 && p.lt_max == 10 && im_roll_enabled()) {
+    // ... and the in-kernel BaseStock / ConstantOrder agents on the 2-role kernel
+    const bool pol_roll = pol && (pol->kind == POL_BASE_STOCK || pol->kind == POL_CONSTANT) && im_pol_roll_enabled();
+    if ((!pol || pol_roll) && io.K > 1 && t_u >= 0 && p.cm.autoreset != AR_SAME_STEP && p.dist == 1 &&
+        !p.cm.info_rec && M1 == 3 && p.L[0] == 1 && p.L[1] == 5 && p.L[2] == 10 && p.lt_max == 10 &&
+        im_roll_enabled()) {
         using G = ImLt3<1, 5, 10>;
         using G3 = ImLt3o<1, 5, 10>;
         const dim3 g3(grid_for(p.cm.N, WAVE));
+        if (pol) {
+            if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
+            else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
+            return hipGetLastError();
+        }
         // up to one 2-role workgroup per SIMD pair (N <= 32768): the dynamics
         // wave's chain is the step time, so split it (measured on MI355X:
         // LostSales 32768 envs 87.5 -> 77.7 us per K = 30; at 65536 the
@@ -1634,8 +1717,8 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
             if (backlog) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, true>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io);
             else hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, false>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io);
         } else {
-            if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io);
-            else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io);
+            if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true, false>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
+            else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false, false>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
         }
         return hipGetLastError();
     }

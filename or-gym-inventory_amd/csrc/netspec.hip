@@ -1081,9 +1081,14 @@ struct NetRoll3 {
     static constexpr size_t lds() { return tile_bytes() + rhs_bytes() + dbuf_bytes() + ring_bytes() + rec_bytes(); }
 };
 
-template <class G, int CH_>
+// POL (invsim_rollout_policy with CONSTANT, ConstantOrderAgent,
+// benchmark_NetInvMgmtBacklogEnv.py:119-135): the dynamics wave takes the
+// agent's fixed order instead of loading actions, every output is optional,
+// and the evaluate_agent sums accumulate in registers (spec_core, as
+// net_spec_kernel).
+template <class G, int CH_, bool POL>
 __global__ void __launch_bounds__(3 * WAVE)
-net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
+net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     using R3 = NetRoll3<G, CH_>;
     using LP = NetLpos<G>;
     constexpr int O = G::O, CH = R3::CH, RD = R3::RD, RL = G::RL, NR = R3::NR;
@@ -1188,7 +1193,7 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
                 }
                 wave_lds_sync();
 #ifndef INVSIM_ABL_ROLL_NO_STORE
-                store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+                if (!POL || io.obs) store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
 #endif
                 wave_lds_sync();
             }
@@ -1214,7 +1219,11 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
     }
     float nact[G::E];
 #pragma unroll
-    for (int k = 0; k < G::E; k++) nact[k] = io.act[el * G::E + k];
+    for (int k = 0; k < G::E; k++) nact[k] = POL ? pol.cf[k] : io.act[el * G::E + k];
+    constexpr int MD = 5 + G::J;             // metrics: reward, steps, demand, sales, stockout, X per node
+    double met[MD];
+#pragma unroll
+    for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
     double napow = P.alpha_pow[t < P.T ? t : 0];
     double dlast[RL];
 #pragma unroll
@@ -1236,7 +1245,7 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
                 const int tn = (t >= P.T) ? 0 : t + 1;          // the next launch step's period
                 napow = P.alpha_pow[tn < P.T ? tn : 0];
             }
-            if (k + 1 < K) {                                    // the next step's actions
+            if (!POL && k + 1 < K) {                            // the next step's actions
 #pragma unroll
                 for (int q = 0; q < G::E; q++) nact[q] = io.act[((int64_t)(k + 1) * N + el) * G::E + q];
             }
@@ -1247,7 +1256,7 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
                 for (int r = 0; r < RL; r++) st.U[r] = 0.0;
 #pragma unroll
                 for (int q = 0; q < G::E; q++) st.Y[q] = 0.0;
-                if (valid) {
+                if (valid && (!POL || io.rew)) {
                     out_store(io.rew + oi, 0.0);
                     out_store(io.term + oi, (uint8_t)0);
                     out_store(io.trunc + oi, (uint8_t)0);
@@ -1266,7 +1275,15 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
                     const double v = rg[(G::ring_off[q] + (int)((uint32_t)t % (uint32_t)G::L[q])) * WAVE];
                     wa[q] = (t >= G::L[q]) ? v : 0.0;
                 }
-                const double rw = spec_core<G>(P, apow, st, act, Dd, wa, Rn, nullptr, nullptr);
+                const double rw = spec_core<G>(P, apow, st, act, Dd, wa, Rn, POL ? met : nullptr, nullptr);
+                if (POL) {
+                    met[0] += rw;                                       // episode_reward += reward
+                    met[1] += 1.0;
+                    if (valid && pol.act_out) {
+#pragma unroll
+                        for (int q = 0; q < G::E; q++) out_store((float *)pol.act_out + oi * G::E + q, act[q]);
+                    }
+                }
 #pragma unroll
                 for (int q = 0; q < G::E; q++)
                     if (G::L[q] > 0) rg[(G::ring_off[q] + (int)((uint32_t)t % (uint32_t)G::L[q])) * WAVE] = Rn[q];
@@ -1277,7 +1294,7 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
 #pragma unroll
                 for (int q = 0; q < G::E; q++)
                     if (G::L[q] > 0) rb[(kk * NR + RL + G::J + LP::rank(q)) * WAVE + lane] = (float)Rn[q];
-                if (valid) {
+                if (valid && (!POL || io.rew)) {
                     out_store(io.rew + oi, rw);
                     out_store(io.term + oi, (uint8_t)0);
                     out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.T ? 1 : 0));
@@ -1311,6 +1328,10 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io) {
         if (P.cm.info_demand && last_real) {
 #pragma unroll
             for (int r = 0; r < RL; r++) P.cm.info_demand[e * RL + r] = (int64_t)dlast[r];
+        }
+        if (POL && pol.metrics) {
+#pragma unroll
+            for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
         }
     }
 }
@@ -1375,6 +1396,12 @@ static bool net_split_enabled() {
     return !(v && v[0] == '0');
 }
 
+// INVSIM_NET_POL_ROLL=0 keeps ConstantOrder rollouts on net_spec_kernel (A/B, tests)
+static bool net_pol_roll_enabled() {
+    const char *v = getenv("INVSIM_NET_POL_ROLL");
+    return !(v && v[0] == '0');
+}
+
 // INVSIM_NET_AHEAD=0 turns the step's demand lookahead off (A/B measurements)
 static bool net_ahead_enabled() {
     const char *v = getenv("INVSIM_NET_AHEAD");
@@ -1419,12 +1446,18 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
         if (ph) hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL, PhiloxGen>), grid, block, lds, s, p, t_u, io, pv); \
         else hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL, Pcg>), grid, block, lds, s, p, t_u, io, pv);         \
     } while (0)
-    if (!ph && !pol && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
+    // ... and the in-kernel ConstantOrder agent on the 3-role kernel
+    const bool pol_roll = pol && pol->kind == POL_CONSTANT && net_pol_roll_enabled();
+    if (!ph && (!pol || pol_roll) && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
         (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
         const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE));
+        using R3 = NetRoll3<G, NET_ROLL3_CH>;
+        if (pol) {
+            hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, true>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv);
+            return hipGetLastError();
+        }
         if (net_roll3_use(p.cm.N)) {
-            using R3 = NetRoll3<G, NET_ROLL3_CH>;
-            hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io);
+            hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, false>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv);
         } else {
             hipLaunchKernelGGL((net_roll_kernel<G>), gr, dim3(2 * WAVE), NetRoll<G>::lds(), s, p, t_u, io);
         }

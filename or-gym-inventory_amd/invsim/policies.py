@@ -132,7 +132,9 @@ def rollout_policy(env, agent, K, obs=False, rewards=True, actions=False, metric
         out["reward"] = torch.empty((K, N), dtype=torch.float64, device=dev)
         out["terminated"] = torch.empty((K, N), dtype=torch.bool, device=dev)
         out["truncated"] = torch.empty((K, N), dtype=torch.bool, device=dev)
-    a = torch.empty((K, N, env.action_dim), dtype=env.act_dtype, device=dev) if actions else None
+    # the kernels record the agent's order of every stepped env; a NEXT_STEP
+    # reset step (whose action the env ignores) keeps the 0 written here
+    a = torch.zeros((K, N, env.action_dim), dtype=env.act_dtype, device=dev) if actions else None
     p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     _capi.check(env._lib.invsim_rollout_policy(
         env._h, int(K), C.byref(spec), p(o), p(out.get("reward")), p(out.get("terminated")),

@@ -414,3 +414,64 @@ def test_summary_table_matches_reference_aggregation():
         assert row["SuccessfulEpisodes"] == len(x) == row["EpisodesAttempted"]
         assert row["SuccessRate(%)"] == 100.0
     assert list(t.index) == sorted(t.index, key=lambda a: -t.loc[a, "AvgReward"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls", ["InvManagementBacklogEnv", "InvManagementLostSalesEnv"])
+@pytest.mark.parametrize("agent", ["base_stock_1.0", "base_stock_1.3", "constant"])
+@pytest.mark.parametrize("n", [4096, 65536])
+def test_policy_on_fused_rollout_equals_run_kernel(gpu, monkeypatch, cls, agent, n):
+    """BaseStock / ConstantOrder inside the fused 2-role rollout kernel
+    (im_roll3_kernel<..., POL>) give the one-wave run kernel's outputs, actions,
+    metrics and final state bit for bit, across NEXT_STEP autoresets and
+    chained launches (every output optional)."""
+    import torch
+    import invsim
+    ag = invsim.ConstantOrderAgent(0.3) if agent == "constant" else invsim.BaseStockAgent(float(agent[-3:]))
+    res = []
+    for roll in ("1", "0"):
+        monkeypatch.setenv("INVSIM_IM_POL_ROLL", roll)
+        env = getattr(invsim, cls)(n, device=gpu)
+        env.reset(seed=21)
+        m = torch.zeros((n, 6), dtype=torch.float64, device=gpu)
+        a = env.rollout_policy(ag, 45, obs=True, actions=True, metrics=m)
+        b = env.rollout_policy(ag, 40, obs=False, rewards=False, metrics=m)
+        c = env.rollout_policy(ag, 30, obs=True, metrics=m)
+        res.append((a, b, c, m, env.get_state()))
+    (a1, b1, c1, m1, s1), (a2, b2, c2, m2, s2) = res
+    for k in a1:
+        assert torch.equal(a1[k], a2[k]), k
+    for k in c1:
+        assert torch.equal(c1[k], c2[k]), k
+    assert torch.equal(m1.view(torch.int64), m2.view(torch.int64))
+    assert torch.equal(s1, s2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", ["default", "custom"])
+@pytest.mark.parametrize("n", [4096, 32768])
+def test_constant_order_on_fused_net_rollout_equals_spec_kernel(gpu, monkeypatch, graph, n):
+    """ConstantOrder inside the 3-role Net rollout kernel (net_roll3o_kernel<...,
+    POL>) gives net_spec_kernel's outputs, actions, metrics and state bit for bit."""
+    import torch
+    import invsim
+    from invsim.topology import custom_graph, default_graph
+    ag = invsim.ConstantOrderAgent(0.15)
+    res = []
+    for roll in ("1", "0"):
+        monkeypatch.setenv("INVSIM_NET_POL_ROLL", roll)
+        g = default_graph() if graph == "default" else custom_graph()
+        env = invsim.NetInvMgmtBacklogEnv(n, device=gpu, graph=g)
+        env.reset(seed=8)
+        m = torch.zeros((n, invsim.policies.metrics_dim(env)), dtype=torch.float64, device=gpu)
+        a = env.rollout_policy(ag, 45, obs=True, actions=True, metrics=m)
+        b = env.rollout_policy(ag, 40, obs=False, rewards=False, metrics=m)
+        c = env.rollout_policy(ag, 30, obs=True, metrics=m)
+        res.append((a, b, c, m, env.get_state()))
+    (a1, b1, c1, m1, s1), (a2, b2, c2, m2, s2) = res
+    for k in a1:
+        assert torch.equal(a1[k], a2[k]), k
+    for k in c1:
+        assert torch.equal(c1[k], c2[k]), k
+    assert torch.equal(m1.view(torch.int64), m2.view(torch.int64))
+    assert torch.equal(s1, s2)
