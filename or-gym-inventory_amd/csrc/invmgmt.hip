@@ -1264,20 +1264,26 @@ struct ImLt3o : ImLt3<L0, L1, L2> {
     static constexpr int CH = IM_ROLL3O_CH;                              // chunk (launch steps)
     static constexpr int RD = IM_ROLL3O_RD;                              // demand ring depth (chunks)
     static constexpr int M1 = 3, O = ImLt3<L0, L1, L2>::O;
-    static constexpr size_t lds() {
-        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + 2 * CH * M1 * WAVE * 8;
+    // POL adds abuf [2][CH][M1][WAVE]: the agent's orders, dynamics -> obs wave
+    static constexpr size_t lds(bool pol = false) {
+        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + (pol ? 4 : 2) * CH * M1 * WAVE * 8;
     }
 };
 
-template <int L0, int L1, int L2, bool BACKLOG>
+// POL (invsim_rollout_policy, BASE_STOCK / CONSTANT): the dynamics wave
+// computes each step's order from I and its own register history of the last
+// L_i orders per stage (hv), and hands the orders to the obs wave in LDS (abuf)
+// beside the inventory; outputs optional, metrics in registers (as im_roll3_kernel).
+template <int L0, int L1, int L2, bool BACKLOG, bool POL>
 __global__ void __launch_bounds__(3 * WAVE)
-im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
+im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     using G = ImLt3o<L0, L1, L2>;
     constexpr int M1 = G::M1, D = G::D, O = G::O, CH = G::CH;
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
     double *rhs_l = reinterpret_cast<double *>(im_tile + WAVE * O);
     int64_t *dbuf = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);   // [RD * CH][WAVE]
     int64_t *ibuf = dbuf + G::RD * CH * WAVE;                             // [2][CH][M1][WAVE]
+    int64_t *abuf = ibuf + 2 * CH * M1 * WAVE;                            // POL: [2][CH][M1][WAVE]
     const int lane = threadIdx.x & (WAVE - 1);
     const int role = threadIdx.x / WAVE;
     const int64_t N = P.cm.N;
@@ -1323,17 +1329,18 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
         }
         int64_t nact[M1];
 #pragma unroll
-        for (int i = 0; i < M1; i++) nact[i] = io.act[el * M1 + i];
+        for (int i = 0; i < M1; i++) nact[i] = POL ? 0 : io.act[el * M1 + i];
         wg_lds_sync();   // barrier 0
         for (int c = 0; c < nch; c++) {
             wg_lds_sync();   // barrier c + 1: inventory chunk c ready
             const int64_t *ib = ibuf + (c & 1) * CH * M1 * WAVE;
+            const int64_t *ab = abuf + (c & 1) * CH * M1 * WAVE;
             for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
                 const int k = c * CH + kk;
                 int64_t req[M1];
 #pragma unroll
-                for (int i = 0; i < M1; i++) req[i] = nact[i];
-                if (k + 1 < K) {                       // the next step's actions
+                for (int i = 0; i < M1; i++) req[i] = POL ? ab[(kk * M1 + i) * WAVE + lane] : nact[i];
+                if (!POL && k + 1 < K) {               // the next step's actions
 #pragma unroll
                     for (int i = 0; i < M1; i++) nact[i] = io.act[((int64_t)(k + 1) * N + el) * M1 + i];
                 }
@@ -1381,8 +1388,9 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 }
                 wave_lds_sync();
 #ifndef INVSIM_ABL_ROLL_NO_STORE
-                store_tile<(O * WAVE * 8 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + ((int64_t)k * N + e0) * O,
-                                                                        (int64_t)nvalid * O, lane);
+                if (!POL || io.obs)
+                    store_tile<(O * WAVE * 8 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + ((int64_t)k * N + e0) * O,
+                                                                            (int64_t)nvalid * O, lane);
 #endif
                 wave_lds_sync();
             }
@@ -1409,7 +1417,19 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
     }
     int64_t nact[M1];
 #pragma unroll
-    for (int i = 0; i < M1; i++) nact[i] = io.act[el * M1 + i];
+    for (int i = 0; i < M1; i++) nact[i] = POL ? 0 : io.act[el * M1 + i];
+    // POL: hv[i][a] = action_log[t - 1 - a, i], the last W(i) requested orders of stage i
+    int64_t hv[M1][D > 0 ? D : 1];
+#pragma unroll
+    for (int i = 0; i < M1; i++) {
+#pragma unroll
+        for (int a = 0; a < G::W(i); a++)
+            hv[i][a] = POL ? alog_get(P, ((int64_t)((uint32_t)(t - 1 - a + 256 * D) % (uint32_t)D) * S + el) * M1 + i) : 0;
+    }
+    constexpr int MD = 6;                                 // metrics (invsim.h INVSIM_METRICS_*)
+    double met[MD];
+#pragma unroll
+    for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
     double napow = P.alpha_pow[t < P.periods ? t : 0];   // alpha**t of the next step, prefetched
     int64_t dlast = 0;
     bool last_real = false;
@@ -1417,6 +1437,7 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
     for (int c = 0; c < nch; c++) {
         const int64_t *db = dbuf + (c % G::RD) * CH * WAVE;
         int64_t *ib = ibuf + (c & 1) * CH * M1 * WAVE;
+        int64_t *ab = abuf + (c & 1) * CH * M1 * WAVE;
         for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
             const int k = c * CH + kk;
             const int64_t oi = (int64_t)k * N + e;
@@ -1428,7 +1449,7 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 const int tn = (t >= P.periods) ? 0 : t + 1;     // the next launch step's period
                 napow = P.alpha_pow[tn < P.periods ? tn : 0];
             }
-            if (k + 1 < K) {                       // prefetch the next step's actions
+            if (!POL && k + 1 < K) {               // prefetch the next step's actions
 #pragma unroll
                 for (int i = 0; i < M1; i++) nact[i] = io.act[((int64_t)(k + 1) * N + el) * M1 + i];
             }
@@ -1439,7 +1460,7 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 for (int q = 0; q <= M1; q++) B[q] = 0;
 #pragma unroll
                 for (int i = 0; i < M1; i++) ib[(kk * M1 + i) * WAVE + lane] = I[i];
-                if (valid) {
+                if (valid && (!POL || io.rew)) {
                     out_store(io.rew + oi, 0.0);
                     out_store(io.term + oi, (uint8_t)0);
                     out_store(io.trunc + oi, (uint8_t)0);
@@ -1447,6 +1468,32 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 t = 0;
             } else {
                 const int64_t d = db[kk * WAVE + lane];
+                if (POL) {
+                    if (pol.kind == POL_BASE_STOCK) {   // im_base_stock from the register history
+#pragma unroll
+                        for (int i = 0; i < M1; i++) {
+                            int64_t pos = I[i];                                 // observation[:M1] = I[t]
+                            int64_t pipe = 0;
+#pragma unroll
+                            for (int a = 0; a < G::lt(i); a++)                  // action_log[max(0, t - L_i) : t, i]
+                                if (t - 1 - a >= 0) pipe = wrap_add(pipe, hv[i][a]);
+                            if (G::lt(i) > 0) pos = wrap_add(pos, pipe);
+                            const double target = ((double)(G::lt(i) + 1) * pol.mu) * pol.sf;
+                            double x = target - (double)pos;
+                            x = (x > 0) ? x : 0.0;                              // np.maximum(0, .)
+                            x = (x < 0.0) ? 0.0 : x;                            // np.clip(., 0, c)
+                            x = (x > (double)P.c[i]) ? (double)P.c[i] : x;
+                            req[i] = (int64_t)x;
+                        }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < M1; i++) req[i] = pol.ci[i];
+                    }
+                    if (valid && pol.act_out) {
+#pragma unroll
+                        for (int i = 0; i < M1; i++) out_store((int64_t *)pol.act_out + oi * M1 + i, req[i]);
+                    }
+                }
                 int64_t ordreq[M1], R[M1], Icur[M1];
 #pragma unroll
                 for (int i = 0; i < M1; i++) req[i] = req[i] > 0 ? req[i] : 0;   // :250
@@ -1485,6 +1532,24 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                 }
                 const double profit = np_sum<double>(M1 + 1, [&](int q) { return term[q]; });
                 const double reward = apow * profit;                            // :322
+                if (POL) {   // evaluate_agent metrics (benchmark_InvManagementBacklogEnv.py:378-399)
+                    met[2] += (double)d;                                        // demand_realized
+                    met[3] += (double)Sv[0];                                    // sales[0]
+                    met[4] += (double)U[0];                                     // unfulfilled[0]
+                    int64_t es = 0;                                             // sum(max(0, ending_inventory))
+#pragma unroll
+                    for (int i = 0; i < M1; i++) es = wrap_add(es, Icur[i] > 0 ? Icur[i] : 0);
+                    met[5] += (double)es;
+                    met[0] += reward;                                           // episode_reward += reward
+                    met[1] += 1.0;                                              // episode_steps
+#pragma unroll
+                    for (int i = 0; i < M1; i++) {
+                        ab[(kk * M1 + i) * WAVE + lane] = req[i];               // the order -> obs wave
+#pragma unroll
+                        for (int a = G::W(i) - 1; a >= 1; a--) hv[i][a] = hv[i][a - 1];
+                        hv[i][0] = req[i];
+                    }
+                }
 #pragma unroll
                 for (int i = 0; i < M1; i++) ib[(kk * M1 + i) * WAVE + lane] = Icur[i];   // obs I (:366)
                 // the new fulfilled-order ring slots R[t] (:267)
@@ -1494,9 +1559,11 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
                         const int L = G::lt(i);
                         if (L > 0) st_store(P.Rring + (int64_t)(P.ring_off[i] + (int)((uint32_t)t % (uint32_t)L)) * S + e, R[i]);
                     }
-                    out_store(io.rew + oi, reward);
-                    out_store(io.term + oi, (uint8_t)0);
-                    out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.periods ? 1 : 0));   // :350
+                    if (!POL || io.rew) {
+                        out_store(io.rew + oi, reward);
+                        out_store(io.term + oi, (uint8_t)0);
+                        out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.periods ? 1 : 0));   // :350
+                    }
                 }
                 // age the windows by one period
 #pragma unroll
@@ -1527,6 +1594,10 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io) {
             for (int q = 0; q <= M1; q++) st_store(P.B + q * S + e, B[q]);
         }
         if (P.cm.info_demand && last_real) P.cm.info_demand[e] = dlast;
+        if (POL && pol.metrics) {
+#pragma unroll
+            for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
+        }
     }
 }
 
@@ -1705,8 +1776,13 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
         using G3 = ImLt3o<1, 5, 10>;
         const dim3 g3(grid_for(p.cm.N, WAVE));
         if (pol) {
-            if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
-            else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
+            if (p.cm.N <= im_roll3o_max_n()) {
+                if (backlog) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, true, true>), g3, dim3(3 * WAVE), G3::lds(true), s, p, t_u, io, pv);
+                else hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, false, true>), g3, dim3(3 * WAVE), G3::lds(true), s, p, t_u, io, pv);
+            } else {
+                if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
+                else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
+            }
             return hipGetLastError();
         }
         // up to one 2-role workgroup per SIMD pair (N <= 32768): the dynamics
@@ -1714,8 +1790,8 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
         // LostSales 32768 envs 87.5 -> 77.7 us per K = 30; at 65536 the
         // 2-role kernel is faster, 118 vs 152 us)
         if (p.cm.N <= im_roll3o_max_n()) {
-            if (backlog) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, true>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io);
-            else hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, false>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io);
+            if (backlog) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, true, false>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io, pv);
+            else hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, false, false>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io, pv);
         } else {
             if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true, false>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
             else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false, false>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
