@@ -13,8 +13,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROLL_KERNELS = {"invmgmt_backlog": "im_roll3_kernel", "invmgmt_lostsales": "im_roll3o_kernel",
                 "newsvendor": "nv_roll_kernel", "net_backlog": "net_roll3o_kernel"}
-POL_KERNELS = {"invmgmt_backlog": "im_run_kernel", "invmgmt_lostsales": "im_run_kernel",
-               "newsvendor": "nv_run_kernel", "net_backlog": "net_spec_kernel"}
+POL_KERNELS = {"invmgmt_backlog": "im_roll3_kernel", "invmgmt_lostsales": "im_roll3o_kernel",
+               "newsvendor": "nv_run_kernel", "net_backlog": "net_roll3o_kernel"}
 KERNELS = {"invmgmt_backlog": "im_split_kernel", "invmgmt_lostsales": "im_split_kernel",
            "newsvendor": "nv_step1_kernel", "net_backlog": "net_step2_kernel"}
 
@@ -80,7 +80,7 @@ def main():
                         f"{r['frac']:.3f} | "
                         + (f"{pm['rocprof_kernel_ns_mean'] / 1e3:.2f} | {pm['traffic_over_algorithmic']:.2f} |"
                            if pm and pm.get('traffic_over_algorithmic') else
-                           f"{(kernel_avg_ns(os.path.join(dst, f'{wl}_rollout_kernel_stats.csv'), ROLL_KERNELS[wl]) or float('nan')) / 1e3:.2f} | |"))
+                           f"{(kernel_avg_ns(os.path.join(dst, f'{wl}_{mode}_kernel_stats.csv'), (ROLL_KERNELS if mode == 'rollout' else POL_KERNELS)[wl]) or float('nan')) / 1e3:.2f} | |"))
     sq = os.path.join(src, "sq_newsvendor")
     if os.path.isdir(sq):
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "sq_summary.py"), sq,
