@@ -894,9 +894,12 @@ struct NvRoll {
     }
 };
 
-template <int LT>
+// POL (invsim_rollout_policy): the dynamics wave asks the agent for each
+// step's order (OrderUpTo / ClassicNV / (s, S) / Constant, as nv_run_kernel)
+// instead of loading it; every output optional, the per-env sums in registers.
+template <int LT, bool POL>
 __global__ void __launch_bounds__(3 * WAVE)
-nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
+nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     using R = NvRoll<LT>;
     constexpr int O = R::O, CH = R::CH, NP = R::NP;
     constexpr int TILE_IT = (EPW * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
@@ -1043,13 +1046,19 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
             if (!(p >= LT - sc)) st.pv[p] = 0.f;
         }
     }
-    float nact = io.act[el];
+    float nact = POL ? 0.f : io.act[el];
+    constexpr int MD = 2;                       // metrics: reward sum, steps
+    double met[MD];
+#pragma unroll
+    for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
+    double lvl = 0.0;     // CLASSIC_NV / SS: the episode's ppf level, once computed
+    bool have = false;
     int kk = 0, cb = 0;
     nv_wg_sync();   // barrier 0: chunk 0 ready
     for (int k = 0; k < K; k++) {
         const int64_t oi = (int64_t)k * N + e;
-        const float act = nact;
-        if (k + 1 < K) nact = io.act[(int64_t)(k + 1) * N + el];   // the next step's action
+        float act = nact;
+        if (!POL && k + 1 < K) nact = io.act[(int64_t)(k + 1) * N + el];   // the next step's action
         const bool rs = nxt && sc >= P.step_limit;
         if (rs) {                                                  // NEXT_STEP autoreset
 #pragma unroll
@@ -1059,19 +1068,31 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
             obs_params(st.par, trow);
 #pragma unroll
             for (int j = 0; j < LT; j++) trow[5 + j] = 0.f;
-            if (valid) {
+            if (valid && (!POL || io.rew)) {
                 out_store(io.rew + oi, 0.0);
                 out_store(io.term + oi, (uint8_t)0);
                 out_store(io.trunc + oi, (uint8_t)0);
             }
+            have = false;
             sc = 0;
         } else {
+            if (POL) {
+                if (pol.kind == POL_ORDER_UP_TO) act = nv_order_up_to<LT>(P, pol, e, sc, st);
+                else if (pol.kind == POL_CLASSIC_NV) act = nv_classic<LT>(P, pol, e, sc, st, lvl, have);
+                else if (pol.kind == POL_SS) act = nv_ss<LT>(P, pol, e, sc, st, lvl, have);
+                else act = pol.cf[0];
+                if (valid && pol.act_out) out_store((float *)pol.act_out + oi, act);
+            }
             const int64_t d = dbuf[(cb * CH + kk) * WAVE + lane];
             double r;
             const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, lg_l, nullptr, r,
                                              (valid && k == K - 1) ? P.cm.info_demand : nullptr, d,
                                              (valid && k == K - 1) ? (double *)P.cm.info_rec : nullptr);
-            if (valid) {
+            if (POL) {
+                met[0] += r;                    // episode_reward += reward (benchmark_newsvendor.py:241)
+                met[1] += 1.0;
+            }
+            if (valid && (!POL || io.rew)) {
                 out_store(io.rew + oi, r);
                 out_store(io.term + oi, (uint8_t)0);
                 out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
@@ -1080,7 +1101,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
         }
         wave_lds_sync();
 #ifndef INVSIM_ABL_ROLL_NO_STORE
-        store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+        if (!POL || io.obs) store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
 #endif
         wave_lds_sync();
         if (++kk == CH || rs || k == K - 1) {      // chunk consumed
@@ -1088,6 +1109,10 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io) {
             kk = 0;
             cb ^= 1;
         }
+    }
+    if (POL && valid && pol.metrics) {
+#pragma unroll
+        for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
     }
 }
 
@@ -1105,6 +1130,12 @@ __global__ void __launch_bounds__(256) nv_commit_kernel(NvParams P, int slot) {
     const uint64_t *A = P.ahead + (int64_t)slot * 3 * S;
     P.cm.rng.hi[e] = A[e];
     P.cm.rng.lo[e] = A[S + e];
+}
+
+// INVSIM_NV_POL_ROLL=0 keeps policy rollouts on nv_run_kernel (A/B measurements, tests)
+inline bool nv_pol_roll_enabled() {
+    const char *v = getenv("INVSIM_NV_POL_ROLL");
+    return !(v && v[0] == '0');
 }
 
 // INVSIM_NV_AHEAD=0 turns the demand lookahead off (A/B measurements)
@@ -1200,13 +1231,16 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
         ahead = false;
         if (ce != hipSuccess) return ce;
     }
-    if (!ph && !pol && io.K > 1 && t_u >= 0 && p.L > 0 && p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
+    if (!ph && (!pol || nv_pol_roll_enabled()) && io.K > 1 && t_u >= 0 && p.L > 0 &&
+        p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
         const dim3 gr(grid_for(p.cm.N, WAVE)), br(3 * WAVE);
         bool done = true;
 #define R_(X)                                                                                              \
     do {                                                                                                   \
-        if (X > 0) hipLaunchKernelGGL((nv_roll_kernel<(X > 0 ? X : 1)>), gr, br, NvRoll<(X > 0 ? X : 1)>::lds(), s, p, t_u, io); \
-        else done = false;                                                                                 \
+        if (X > 0) {                                                                                       \
+            if (pol) hipLaunchKernelGGL((nv_roll_kernel<(X > 0 ? X : 1), true>), gr, br, NvRoll<(X > 0 ? X : 1)>::lds(), s, p, t_u, io, pv); \
+            else hipLaunchKernelGGL((nv_roll_kernel<(X > 0 ? X : 1), false>), gr, br, NvRoll<(X > 0 ? X : 1)>::lds(), s, p, t_u, io, pv); \
+        } else done = false;                                                                               \
     } while (0)
         NV_LT_SWITCH(R_)
 #undef R_

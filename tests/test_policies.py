@@ -475,3 +475,36 @@ def test_constant_order_on_fused_net_rollout_equals_spec_kernel(gpu, monkeypatch
         assert torch.equal(c1[k], c2[k]), k
     assert torch.equal(m1.view(torch.int64), m2.view(torch.int64))
     assert torch.equal(s1, s2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agent", ["order_up_to", "classic_nv", "ss", "constant"])
+@pytest.mark.parametrize("n,L,limit", [(4096, 5, 40), (65536, 5, 40), (5000, 2, 12), (3000, 9, 17)])
+def test_newsvendor_policy_on_fused_rollout_equals_run_kernel(gpu, monkeypatch, agent, n, L, limit):
+    """OrderUpTo / ClassicNV / (s, S) / ConstantOrder inside the 3-wave
+    Newsvendor rollout kernel (nv_roll_kernel<LT, POL>) give nv_run_kernel's
+    outputs, actions, metrics and final state bit for bit, across NEXT_STEP
+    autoresets (the per-episode ppf level recomputed) and chained launches."""
+    import torch
+    import invsim
+    ag = {"order_up_to": lambda: invsim.OrderUpToHeuristicAgent(1.2),
+          "classic_nv": lambda: invsim.ClassicNewsvendorAgent("profit_margin", 0.9),
+          "ss": lambda: invsim.sSPolicyAgent(0.5, 1.4),
+          "constant": lambda: invsim.ConstantOrderAgent(0.05)}[agent]()
+    res = []
+    for roll in ("1", "0"):
+        monkeypatch.setenv("INVSIM_NV_POL_ROLL", roll)
+        env = invsim.NewsvendorEnv(n, device=gpu, lead_time=L, step_limit=limit)
+        env.reset(seed=31)
+        m = torch.zeros((n, 2), dtype=torch.float64, device=gpu)
+        a = env.rollout_policy(ag, 45, obs=True, actions=True, metrics=m)
+        b = env.rollout_policy(ag, 40, obs=False, rewards=False, metrics=m)
+        c = env.rollout_policy(ag, 30, obs=True, metrics=m)
+        res.append((a, b, c, m, env.get_state()))
+    (a1, b1, c1, m1, s1), (a2, b2, c2, m2, s2) = res
+    for k in a1:
+        assert torch.equal(a1[k], a2[k]), k
+    for k in c1:
+        assert torch.equal(c1[k], c2[k]), k
+    assert torch.equal(m1.view(torch.int64), m2.view(torch.int64))
+    assert torch.equal(s1, s2)

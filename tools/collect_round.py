@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROLL_KERNELS = {"invmgmt_backlog": "im_roll3_kernel", "invmgmt_lostsales": "im_roll3o_kernel",
                 "newsvendor": "nv_roll_kernel", "net_backlog": "net_roll3o_kernel"}
 POL_KERNELS = {"invmgmt_backlog": "im_roll3_kernel", "invmgmt_lostsales": "im_roll3o_kernel",
-               "newsvendor": "nv_run_kernel", "net_backlog": "net_roll3o_kernel"}
+               "newsvendor": "nv_roll_kernel", "net_backlog": "net_roll3o_kernel"}
 KERNELS = {"invmgmt_backlog": "im_split_kernel", "invmgmt_lostsales": "im_split_kernel",
            "newsvendor": "nv_step1_kernel", "net_backlog": "net_step2_kernel"}
 
