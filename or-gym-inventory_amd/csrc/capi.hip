@@ -743,7 +743,8 @@ int invsim_set_info_demand(invsim_handle *h, int64_t *demand) {
 
 // bring cm.rng up to date from the demand lookahead cache (the cache stays valid)
 static int commit_rng(invsim_handle *h, hipStream_t s) {
-    if (!h->la_valid) return INVSIM_OK;
+    // a fast-stream cache holds demands only (set_demand_stream drops the other kind)
+    if (!h->la_valid || h->demand_stream == INVSIM_DEMAND_PHILOX) return INVSIM_OK;
     hipError_t e = hipSuccess;
     if (h->family == INVSIM_INVMGMT) e = im_commit_launch(h->im, h->la_slot, s);
     else if (h->family == INVSIM_NEWSVENDOR) e = nv_commit_launch(h->nv, h->la_slot, s);

@@ -93,6 +93,27 @@ struct PhiloxGen {
     }
 };
 
+// A stream wave's draw position (stream_flat_loop): the fast stream is put at
+// draw r of launch step j before each attempt (a PTRS rejection continues the
+// same (j, r) block sequence, as the run kernels' set_step + sub); a
+// sequential stream simply continues.
+template <class G>
+struct StreamPos {
+    uint64_t base;             // the handle's launch-step counter (Common::ph_step)
+    int j = -1, r = -1;
+    __device__ __forceinline__ explicit StreamPos(uint64_t b) : base(b) {}
+    __device__ __forceinline__ void at(G &g, int jj, int rr) {
+        if constexpr (G::kCounter) {
+            if (jj != j || rr != r) {
+                g.set_step(base + (uint64_t)jj);
+                g.sub((uint32_t)rr);
+                j = jj;
+                r = rr;
+            }
+        }
+    }
+};
+
 // ---------------------------------------------------------------- SeedSequence
 __device__ __forceinline__ uint32_t ss_hashmix(uint32_t v, uint32_t &hc) {
     v ^= hc;

@@ -607,7 +607,10 @@ __device__ __forceinline__ void wg_lds_sync() {
 // which the host flips to `cur ^ 1` of the new current slot; cm.rng is brought
 // up to date from it (im_commit_kernel) only before something reads it: another
 // kernel, get_state, a masked seed.
-template <int M1, bool BACKLOG, bool NPD, bool AHEAD>
+// RG = PhiloxGen (the fast stream, invmgmt_ph.hip): the same lookahead, but a
+// draw is a function of (key, launch step) only, so the cache holds just the
+// next step's demand (row 2 of a slot) and no generator state is read or written.
+template <int M1, bool BACKLOG, bool NPD, bool AHEAD, class RG = Pcg>
 __global__ void __launch_bounds__(2 * WAVE)
 im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0, int gla) {
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
@@ -627,7 +630,7 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         for (int u = 0; u < TableStage::NT; u++) ts.v[u] = tsrc[min(lane + u * WAVE, qm)];
         return ts;
     };
-    auto draw = [&](Pcg &g, uint64_t &u32) -> int64_t {
+    auto draw = [&](auto &g, uint64_t &u32) -> int64_t {
 #ifdef INVSIM_ABL_NO_POISSON  // profiling ablation build only (wrong results)
         int64_t x = 20 + (int64_t)(g.lo & 3);
         g.next64();
@@ -644,6 +647,17 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         const bool valid = e < N;
         const int64_t ee = valid ? e : N - 1;
         TableStage ts = stage_table((int)(threadIdx.x & (WAVE - 1)));
+        if constexpr (RG::kCounter) {   // the fast stream: the draw of launch step ph_step + 1
+            RG g;
+            P.cm.rng.load(ee, g);
+            g.set_step(P.cm.ph_step + 1);
+            g.sub(0);
+            uint64_t u32 = 0;
+            ts.flush((int)(threadIdx.x & (WAVE - 1)));
+            const int64_t dn = draw(g, u32);
+            if (valid) st_store(Anxt + 2 * S + e, (uint64_t)dn);
+            return;
+        }
         Pcg g;
         g.hi = Acur[ee];
         g.lo = Acur[S + ee];
@@ -695,15 +709,17 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
     if (demand_wave) {
         const int64_t ee = valid ? e : N - 1;        // padded lanes: the last env's stream
         TableStage ts;
-        Pcg g;
+        RG g;
         uint64_t u32 = 0;
         int64_t d = 0;
         if (AHEAD) {
             d = (int64_t)Acur[2 * S + ee];
         } else {
             ts = stage_table(lane);
-            g = P.cm.rng.load(ee);
-            if (NPD) u32 = P.cm.u32buf[ee];
+            P.cm.rng.load(ee, g);
+            g.set_step(P.cm.ph_step);
+            g.sub(0);
+            if (NPD && !RG::kCounter) u32 = P.cm.u32buf[ee];
         }
         // window rows t+1-n .. t-1 (:380), loaded whole (see im_step_regs)
         const int slot0 = D > 0 ? (int)((uint32_t)(t1 - n) % (uint32_t)D) : 0;
@@ -750,26 +766,35 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
             }
         }
         wg_lds_sync();   // d and the window rows -> dynamics wave
-        if (!AHEAD && valid) {   // committed generator state: after this step's draw
-            if (Acur) {          // into slot cur (the committed slot once the slots flip)
-                st_store(Acur + e, g.hi);
-                st_store(Acur + S + e, g.lo);
-                if (NPD) st_store(Acur + 3 * S + e, u32);
-            } else {
-                P.cm.rng.store_state(e, g);
-                if (NPD) P.cm.u32buf[e] = u32;
+        if constexpr (!RG::kCounter) {
+            if (!AHEAD && valid) {   // committed generator state: after this step's draw
+                if (Acur) {          // into slot cur (the committed slot once the slots flip)
+                    st_store(Acur + e, g.hi);
+                    st_store(Acur + S + e, g.lo);
+                    if (NPD) st_store(Acur + 3 * S + e, u32);
+                } else {
+                    P.cm.rng.store_state(e, g);
+                    if (NPD) P.cm.u32buf[e] = u32;
+                }
             }
         }
         wg_lds_sync();   // tile complete
         store_tile<(M1 * 11 * WAVE * 8 / 2 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile, io.obs + e0 * O,
                                                                           thalf < tcount ? thalf : tcount, lane);
         if (!AHEAD && Anxt) {    // lookahead after an inline draw (first step after invalidation)
+            if constexpr (RG::kCounter) {
+                g.set_step(P.cm.ph_step + 1);
+                g.sub(0);
+                u32 = 0;
+            }
             const int64_t dn = draw(g, u32);
             if (valid) {
-                st_store(Anxt + e, g.hi);
-                st_store(Anxt + S + e, g.lo);
+                if constexpr (!RG::kCounter) {
+                    st_store(Anxt + e, g.hi);
+                    st_store(Anxt + S + e, g.lo);
+                    if (NPD) st_store(Anxt + 3 * S + e, u32);
+                }
                 st_store(Anxt + 2 * S + e, (uint64_t)dn);
-                if (NPD) st_store(Anxt + 3 * S + e, u32);
             }
         }
         TWAIT();
@@ -909,16 +934,18 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
 // Same arithmetic, in the same order, as im_step_regs.
 // The demand wave of the rollout kernels (stream_flat_loop): Poisson demand
 // (:280) of each launch step into the ring dbuf [RD * CH][WAVE], nb barriers
-template <int CH, int RD>
-__device__ __forceinline__ void im_stream_loop(const ImParams &P, Pcg &g, const double *rhs_l, int64_t *dbuf,
+template <int CH, int RD, class RG>
+__device__ __forceinline__ void im_stream_loop(const ImParams &P, RG &g, const double *rhs_l, int64_t *dbuf,
                                                int lane, int K, int nb, int t_start) {
+    StreamPos<RG> pos(P.cm.ph_step);
     stream_flat_loop<CH, RD, 1>(
         K, nb, t_start, P.periods,
-        [&](int, int64_t &d) {
+        [&](int j, int, int64_t &d) {
 #ifdef INVSIM_ABL_ROLL_NO_DRAW
             d = 20;
             return true;
 #else
+            pos.at(g, j, 0);
             return np_poisson_try(g, P.pc, rhs_l, d);
 #endif
         },
@@ -946,7 +973,7 @@ struct ImLt3 {
 // window it already holds (plus the age-D row, wold) -- every output is
 // optional, and the evaluate_agent sums accumulate in registers (as
 // im_launch_step / im_step_regs, same order).
-template <int L0, int L1, int L2, bool BACKLOG, bool POL>
+template <int L0, int L1, int L2, bool BACKLOG, bool POL, class RG = Pcg>
 __global__ void __launch_bounds__(2 * WAVE)
 im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     using G = ImLt3<L0, L1, L2>;
@@ -974,7 +1001,8 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO p
 #pragma unroll
             for (int u = 0; u < TableStage::NT; u++) ts.v[u] = tsrc[min(lane + u * WAVE, qm)];
         }
-        Pcg g = P.cm.rng.load(el);
+        RG g;
+        P.cm.rng.load(el, g);
         ts.flush(lane);
         im_stream_loop<CH, G::RD>(P, g, rhs_l, dbuf, lane, K, nch, t_start);   // barriers 0 .. nch - 1
         if (valid) P.cm.rng.store_state(e, g);
@@ -1274,7 +1302,7 @@ struct ImLt3o : ImLt3<L0, L1, L2> {
 // computes each step's order from I and its own register history of the last
 // L_i orders per stage (hv), and hands the orders to the obs wave in LDS (abuf)
 // beside the inventory; outputs optional, metrics in registers (as im_roll3_kernel).
-template <int L0, int L1, int L2, bool BACKLOG, bool POL>
+template <int L0, int L1, int L2, bool BACKLOG, bool POL, class RG = Pcg>
 __global__ void __launch_bounds__(3 * WAVE)
 im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     using G = ImLt3o<L0, L1, L2>;
@@ -1305,7 +1333,8 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
 #pragma unroll
             for (int u = 0; u < TableStage::NT; u++) ts.v[u] = tsrc[min(lane + u * WAVE, qm)];
         }
-        Pcg g = P.cm.rng.load(el);
+        RG g;
+        P.cm.rng.load(el, g);
         ts.flush(lane);
         // barriers 0 .. nch - 1 (demand chunk c ready), nch (the obs wave's last chunk)
         im_stream_loop<CH, G::RD>(P, g, rhs_l, dbuf, lane, K, nch + 1, t_start);
@@ -1650,6 +1679,51 @@ inline bool im_ahead_enabled() {
     return !(s && s[0] == '0');
 }
 
+// the lock-step split step kernel applies (both streams)
+inline bool im_split_applies(const ImParams &p, int t_u, const PolicyIO *pol, const StepIO<int64_t, int64_t> &io) {
+    return !pol && io.K == 1 && t_u >= 0 && t_u < p.periods && io.obs &&
+           !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.periods) && im_split_enabled();
+}
+
+// the 2-/3-role rollout kernels of the reference's default lead times apply
+// (open loop, or the in-kernel BaseStock / ConstantOrder agents)
+inline bool im_roll_applies(const ImParams &p, int M1, int t_u, const PolicyIO *pol,
+                            const StepIO<int64_t, int64_t> &io) {
+    const bool pol_roll = pol && (pol->kind == POL_BASE_STOCK || pol->kind == POL_CONSTANT) && im_pol_roll_enabled();
+    return (!pol || pol_roll) && io.K > 1 && t_u >= 0 && p.cm.autoreset != AR_SAME_STEP && p.dist == 1 &&
+           !p.cm.info_rec && M1 == 3 && p.L[0] == 1 && p.L[1] == 5 && p.L[2] == 10 && p.lt_max == 10 &&
+           im_roll_enabled();
+}
+
+template <class RG>
+hipError_t im_roll_launch(const ImParams &p, bool backlog, int t_u, const PolicyIO *pol,
+                          const StepIO<int64_t, int64_t> &io, hipStream_t s) {
+    PolicyIO none{};
+    const PolicyIO &pv = pol ? *pol : none;
+    using G = ImLt3<1, 5, 10>;
+    using G3 = ImLt3o<1, 5, 10>;
+    const dim3 g3(grid_for(p.cm.N, WAVE));
+    // up to one 2-role workgroup per SIMD pair (N <= 32768): the dynamics
+    // wave's chain is the step time, so split it (measured on MI355X:
+    // LostSales 32768 envs 87.5 -> 77.7 us per K = 30; at 65536 the
+    // 2-role kernel is faster, 118 vs 152 us)
+    const bool three = p.cm.N <= im_roll3o_max_n();
+#define R_(B, POL)                                                                                                    \
+    do {                                                                                                              \
+        if (three) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, B, POL, RG>), g3, dim3(3 * WAVE), G3::lds(POL), s, p, t_u, io, pv); \
+        else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, B, POL, RG>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);            \
+    } while (0)
+    if (pol) {
+        if (backlog) R_(true, true);
+        else R_(false, true);
+    } else {
+        if (backlog) R_(true, false);
+        else R_(false, false);
+    }
+#undef R_
+    return hipGetLastError();
+}
+
 }  // namespace
 
 #define IM_DISPATCH(M1V, BL, LAUNCH)                                   \
@@ -1669,13 +1743,41 @@ inline bool im_ahead_enabled() {
 // invmgmt_ph.hip: this file compiled a second time for the fast-stream run
 // kernels (a TU of their own, so the two instantiation sets compile in parallel)
 hipError_t im_run_launch_ph(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
-                            const StepIO<int64_t, int64_t> &io, hipStream_t s) {
+                            const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s) {
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = (size_t)EPW * M1 * (p.lt_max + 1) * sizeof(int64_t) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
     const bool npd = p.dist >= 2 && p.dist <= 4;
+    if (im_split_applies(p, t_u, pol, io)) {   // the split step kernel, with the demand-only lookahead
+        const size_t lds2 = lds + WAVE * sizeof(int64_t);
+        ImParams q = p;
+        if (!im_ahead_enabled()) q.ahead = nullptr;
+        const bool hit = ahead && q.ahead;
+        const int gla = hit ? (int)grid_for(p.cm.N, 2 * WAVE) : 0;
+        const dim3 grid2(grid.x + gla), block2(2 * WAVE);
+        const int cur = slot;
+        const int la0 = im_la_last() ? (int)grid.x : 0;
+#define S_(M, B)                                                                                        \
+    do {                                                                                                \
+        if (npd) {                                                                                      \
+            if (hit) hipLaunchKernelGGL((im_split_kernel<M, B, true, true, PhiloxGen>), grid2, block2, lds2, s, q, t_u, io, cur, la0, gla);  \
+            else hipLaunchKernelGGL((im_split_kernel<M, B, true, false, PhiloxGen>), grid2, block2, lds2, s, q, t_u, io, cur, la0, gla);     \
+        } else {                                                                                        \
+            if (hit) hipLaunchKernelGGL((im_split_kernel<M, B, false, true, PhiloxGen>), grid2, block2, lds2, s, q, t_u, io, cur, la0, gla); \
+            else hipLaunchKernelGGL((im_split_kernel<M, B, false, false, PhiloxGen>), grid2, block2, lds2, s, q, t_u, io, cur, la0, gla);    \
+        }                                                                                               \
+    } while (0)
+        IM_DISPATCH(M1, backlog, S_)
+#undef S_
+        ahead = q.ahead != nullptr;   // every env drew launch step ph_step + 1 into slot cur ^ 1
+        if (ahead) slot ^= 1;
+        return hipGetLastError();
+    }
+    // any other launch moves the counter past the cached step: the cache is stale
+    ahead = false;
+    if (im_roll_applies(p, M1, t_u, pol, io)) return im_roll_launch<PhiloxGen>(p, backlog, t_u, pol, io, s);
 #define K_(M, B, TU, ONE, POL)                                                                          \
     do {                                                                                                \
         if (npd)                                                                                        \
@@ -1712,17 +1814,9 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
     const bool npd = p.dist >= 2 && p.dist <= 4;
-    const bool ph = p.cm.philox != 0;       // fast stream: the run kernels only (no lookahead, no demand waves)
-    if (ph) {
-        if (ahead) {                        // the parity stream's lookahead cache ends here
-            const hipError_t ce = im_commit_launch(p, slot, s);
-            ahead = false;
-            if (ce != hipSuccess) return ce;
-        }
-        return im_run_launch_ph(p, M1, backlog, t_u, pol, io, s);
-    }
-    if (!pol && io.K == 1 && t_u >= 0 && t_u < p.periods && io.obs &&
-        !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.periods) && im_split_enabled()) {
+    const bool ph = p.cm.philox != 0;       // fast stream: invmgmt_ph.hip (split / rollout / run kernels, no lookahead)
+    if (ph) return im_run_launch_ph(p, M1, backlog, t_u, pol, io, ahead, slot, s);   // (a cache is the fast stream's)
+    if (im_split_applies(p, t_u, pol, io)) {
         const size_t lds2 = lds + WAVE * sizeof(int64_t);
         const dim3 block2(2 * WAVE);
         ImParams q = p;
@@ -1766,38 +1860,9 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
         if (ce != hipSuccess) return ce;
     }
     // lock-step rollout of the reference's default lead times: register windows
-    // and a demand wave (im_roll3_kernel)
-    // ... and the in-kernel BaseStock / ConstantOrder agents on the 2-role kernel
-    const bool pol_roll = pol && (pol->kind == POL_BASE_STOCK || pol->kind == POL_CONSTANT) && im_pol_roll_enabled();
-    if ((!pol || pol_roll) && io.K > 1 && t_u >= 0 && p.cm.autoreset != AR_SAME_STEP && p.dist == 1 &&
-        !p.cm.info_rec && M1 == 3 && p.L[0] == 1 && p.L[1] == 5 && p.L[2] == 10 && p.lt_max == 10 &&
-        im_roll_enabled()) {
-        using G = ImLt3<1, 5, 10>;
-        using G3 = ImLt3o<1, 5, 10>;
-        const dim3 g3(grid_for(p.cm.N, WAVE));
-        if (pol) {
-            if (p.cm.N <= im_roll3o_max_n()) {
-                if (backlog) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, true, true>), g3, dim3(3 * WAVE), G3::lds(true), s, p, t_u, io, pv);
-                else hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, false, true>), g3, dim3(3 * WAVE), G3::lds(true), s, p, t_u, io, pv);
-            } else {
-                if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
-                else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false, true>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
-            }
-            return hipGetLastError();
-        }
-        // up to one 2-role workgroup per SIMD pair (N <= 32768): the dynamics
-        // wave's chain is the step time, so split it (measured on MI355X:
-        // LostSales 32768 envs 87.5 -> 77.7 us per K = 30; at 65536 the
-        // 2-role kernel is faster, 118 vs 152 us)
-        if (p.cm.N <= im_roll3o_max_n()) {
-            if (backlog) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, true, false>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io, pv);
-            else hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, false, false>), g3, dim3(3 * WAVE), G3::lds(), s, p, t_u, io, pv);
-        } else {
-            if (backlog) hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, true, false>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
-            else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, false, false>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);
-        }
-        return hipGetLastError();
-    }
+    // and a demand wave (im_roll3_kernel / im_roll3o_kernel), open loop or with
+    // the in-kernel BaseStock / ConstantOrder agents
+    if (im_roll_applies(p, M1, t_u, pol, io)) return im_roll_launch<Pcg>(p, backlog, t_u, pol, io, s);
 #define K_(M, B, TU, ONE, POL)                                                                         \
     do {                                                                                                \
         if (npd)                                                                                        \

@@ -324,7 +324,7 @@ __device__ __forceinline__ bool np_poisson_try(G &g, const PtrsConst &c, const d
 // soon as every lane has drawn chunk b, and a lane may draw step j only once
 // the consumer is done with the slot's previous step j - RD*CH (barrier
 // (j / CH - RD) + 1 passed).  A NEXT_STEP reset step (t >= T) draws nothing.
-//   draw(r, k) -> bool: one attempt for draw r; put(slot, r, k): store it
+//   draw(j, r, k) -> bool: one attempt for draw r of launch step j; put(slot, r, k): store it
 template <int CH, int RD, int RL, class Draw, class Put>
 __device__ __forceinline__ void stream_flat_loop(int K, int nb, int t, int T, Draw draw, Put put) {
     static_assert(RD >= 2, "the ring needs two chunks");
@@ -341,7 +341,7 @@ __device__ __forceinline__ void stream_flat_loop(int K, int nb, int t, int T, Dr
                 j++;
             } else {
                 int64_t kd = 0;
-                if (draw(r, kd)) {
+                if (draw(j, r, kd)) {
                     put((j % (RD * CH)), r, kd);
                     if (++r == RL) {
                         r = 0;
@@ -375,9 +375,10 @@ hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_
 // slot (updated) does now
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
                          const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s);
-// the fast-stream (cm.philox) run kernels, invmgmt_ph.hip
+// the fast-stream (cm.philox) kernels, invmgmt_ph.hip; ahead / slot: the
+// fast stream's demand-only lookahead cache (never committed: it holds no state)
 hipError_t im_run_launch_ph(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
-                            const StepIO<int64_t, int64_t> &io, hipStream_t s);
+                            const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s);
 // cm.rng <- the committed generator state held by the lookahead cache (whose
 // current slot is `slot`); needed before anything reads cm.rng while it is valid
 hipError_t im_commit_launch(const ImParams &p, int slot, hipStream_t s);

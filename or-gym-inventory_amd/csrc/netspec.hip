@@ -77,7 +77,7 @@ __device__ __forceinline__ void net_demand_loop(Pcg &g, const PtrsConst (&pc)[G:
     constexpr int RL = G::RL;
     stream_flat_loop<CH, RD, RL>(
         K, nb, t_start, T,
-        [&](int r, int64_t &kd) {
+        [&](int, int r, int64_t &kd) {
             PtrsConst c = pc[0];
             const double *rt = rhs_l;
 #pragma unroll

@@ -149,3 +149,93 @@ def test_fast_stream_newsvendor_and_net_rates(gpu):
     ds = torch.stack([net.step(a)[4]["demand"].double() for _ in range(30)])
     assert abs(float(ds.mean()) - 20.0) < 0.05
     assert abs(float(ds.var()) - 20.0) < 0.5
+
+
+def _im_fast_run(gpu, cls, n, fused, monkeypatch, **kw):
+    import invsim
+    for v in ("INVSIM_IM_SPLIT", "INVSIM_IM_ROLL", "INVSIM_IM_POL_ROLL"):
+        monkeypatch.setenv(v, "1" if fused else "0")
+    env = getattr(invsim, cls)(n, device=gpu, demand_stream="philox", record_demand=True, **kw)
+    env.reset(seed=17)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(4)
+    out = []
+    for k in range(33):                                   # split steps, across the NEXT_STEP reset
+        a = torch.randint(0, 120, (n, 3), device=gpu, generator=g)
+        o, r, te, tr, info = env.step(a)
+        out += [o.clone(), r.clone(), tr.clone(), info["demand"].clone()]
+    acts = torch.randint(0, 120, (45, n, 3), device=gpu, generator=g)
+    out += list(env.rollout(acts))                         # fused rollout
+    m = torch.zeros((n, 6), dtype=torch.float64, device=gpu)
+    pol = env.rollout_policy(invsim.BaseStockAgent(1.1), 40, obs=True, actions=True, metrics=m)
+    out += [pol[k] for k in sorted(pol)] + [m]
+    out.append(env.get_state())
+    return out
+
+
+@pytest.mark.parametrize("cls", ["InvManagementBacklogEnv", "InvManagementLostSalesEnv"])
+@pytest.mark.parametrize("n", [4096, 65536])
+def test_fast_stream_fused_kernels_equal_run_kernel(gpu, monkeypatch, cls, n):
+    """The fast stream on the split step kernel and the 2-/3-role rollout
+    kernels (no lookahead: draws at (key, launch step)) gives the one-wave run
+    kernel's results bit for bit: steps, rollouts, policy rollouts, demands and
+    the state blob."""
+    a = _im_fast_run(gpu, cls, n, True, monkeypatch)
+    b = _im_fast_run(gpu, cls, n, False, monkeypatch)
+    assert len(a) == len(b)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x.view(torch.uint8) if x.dtype == torch.float64 else x,
+                           y.view(torch.uint8) if y.dtype == torch.float64 else y), i
+
+
+@pytest.mark.parametrize("dist,param", [(2, {"n": 40, "p": 0.45}), (3, {"low": 3, "high": 37})])
+def test_fast_stream_split_numpy_samplers_equal_run_kernel(gpu, monkeypatch, dist, param):
+    """Binomial / integers demand (the u32 half not carried on the fast stream)
+    on the split step kernel == the run kernel."""
+    a = _im_fast_run(gpu, "InvManagementBacklogEnv", 3000, True, monkeypatch, dist=dist, dist_param=param)
+    b = _im_fast_run(gpu, "InvManagementBacklogEnv", 3000, False, monkeypatch, dist=dist, dist_param=param)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x, y), i
+
+
+def _switch_seq(gpu, monkeypatch, split):
+    import invsim
+    monkeypatch.setenv("INVSIM_IM_SPLIT", "1" if split else "0")
+    n = 2048
+    env = invsim.InvManagementBacklogEnv(n, device=gpu, record_demand=True)
+    env.reset(seed=23)
+    a = torch.full((n, 3), 15, dtype=torch.int64, device=gpu)
+    out = []
+
+    def steps(k):
+        for _ in range(k):
+            o, r, _, _, info = env.step(a)
+            out.extend([o.clone(), r.clone(), info["demand"].clone()])
+    steps(3)                                    # numpy, its lookahead cache live
+    env.set_demand_stream("philox")
+    steps(4)                                    # fast stream, its demand-only cache live
+    out.append(env.get_state().clone())         # commit_rng must leave the PCG64 states alone
+    steps(2)
+    blob = env.get_state().clone()
+    steps(3)
+    env.set_state(blob)                         # counter from the blob; the cache dropped
+    steps(3)
+    env.set_demand_stream("numpy")
+    steps(4)
+    env.reset(seed=5)
+    env.set_demand_stream("philox")
+    steps(2)
+    out.append(env.get_state().clone())
+    return out
+
+
+def test_fast_stream_lookahead_across_switches_and_checkpoints(gpu, monkeypatch):
+    """The fast stream's demand-only lookahead (split step kernel) against the
+    run kernel over stream switches, get_state / set_state and reseeding: the
+    cache is never committed into the PCG64 states and is dropped whenever the
+    counter or the key moves."""
+    a = _switch_seq(gpu, monkeypatch, True)
+    b = _switch_seq(gpu, monkeypatch, False)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x.view(torch.uint8) if x.dtype == torch.float64 else x,
+                           y.view(torch.uint8) if y.dtype == torch.float64 else y), i
