@@ -71,13 +71,16 @@ __device__ __forceinline__ void spec_demand(RG &g, const PtrsConst (&pc)[G::RL],
 
 // The demand wave of the rollout kernels (stream_flat_loop): the market demands
 // of each launch step, retail-link order, into the ring dbuf [RD * CH][RL][WAVE]
-template <class G, int CH, int RD>
-__device__ __forceinline__ void net_demand_loop(Pcg &g, const PtrsConst (&pc)[G::RL], const double *rhs_l,
-                                                double *dbuf, int lane, int K, int nb, int t_start, int T) {
+template <class G, int CH, int RD, class RG>
+__device__ __forceinline__ void net_demand_loop(RG &g, const PtrsConst (&pc)[G::RL], const double *rhs_l,
+                                                double *dbuf, int lane, int K, int nb, int t_start, int T,
+                                                uint64_t ph_step) {
     constexpr int RL = G::RL;
+    StreamPos<RG> pos(ph_step);
     stream_flat_loop<CH, RD, RL>(
         K, nb, t_start, T,
-        [&](int, int r, int64_t &kd) {
+        [&](int j, int r, int64_t &kd) {
+            pos.at(g, j, r);
             PtrsConst c = pc[0];
             const double *rt = rhs_l;
 #pragma unroll
@@ -660,7 +663,10 @@ net_step1_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
 //                     lookahead production when !HIT)
 // Then both waves store half of the tile.  Lookahead workgroups (HIT) cover 128
 // envs, one per thread.  Same arithmetic as net_spec_kernel.
-template <class G, bool HIT>
+// RG = PhiloxGen (the fast stream): a draw is a function of (key, launch step),
+// so the cache holds only the next step's market demands (rows 2 ..), and no
+// generator state is read or written.
+template <class G, bool HIT, class RG = Pcg>
 __global__ void __launch_bounds__(2 * WAVE)
 net_step2_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) {
     extern __shared__ __attribute__((aligned(16))) float ns_lds[];
@@ -699,6 +705,19 @@ net_step2_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
         const int64_t el = valid ? e : N - 1;
         double tv[RL][NT];
         stage(tv);
+        if constexpr (RG::kCounter) {   // the fast stream: launch step ph_step + 1
+            RG g;
+            P.cm.rng.load(el, g);
+            g.set_step(P.cm.ph_step + 1);
+            flush(tv);
+            double Dd[RL];
+            spec_demand<G>(g, pc, rhs_l, Dd);
+            if (valid) {
+#pragma unroll
+                for (int r = 0; r < RL; r++) st_store(Anxt + (2 + r) * S + e, (uint64_t)(int64_t)Dd[r]);
+            }
+            return;
+        }
         Pcg g;
         g.hi = Acur[el];
         g.lo = Acur[S + el];
@@ -760,7 +779,7 @@ net_step2_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
         return;
     }
     // ---- dynamics wave
-    NetSt<G> st;
+    NetSt<G, RG> st;
     double Dd[RL];
     double tv[RL][NT];
     if (HIT) {
@@ -768,7 +787,8 @@ net_step2_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
         for (int r = 0; r < RL; r++) Dd[r] = (double)(int64_t)Acur[(2 + r) * S + el];
     } else {
         stage(tv);
-        st.g = P.cm.rng.load(el);
+        P.cm.rng.load(el, st.g);
+        st.g.set_step(P.cm.ph_step);
     }
     const double apow = P.alpha_pow[t];
 #pragma unroll
@@ -817,14 +837,20 @@ net_step2_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
         for (int k = 0; k < G::E; k++) st_store(P.Y + k * S + e, st.Y[k]);
     }
     if (!HIT) {   // committed state (after this step's draws) -> slot cur; the lookahead -> slot cur ^ 1
-        if (valid) {
-            st_store((uint64_t *)Acur + e, st.g.hi);
-            st_store((uint64_t *)Acur + S + e, st.g.lo);
+        if constexpr (!RG::kCounter) {
+            if (valid) {
+                st_store((uint64_t *)Acur + e, st.g.hi);
+                st_store((uint64_t *)Acur + S + e, st.g.lo);
+            }
+        } else {
+            st.g.set_step(P.cm.ph_step + 1);
         }
         spec_demand<G>(st.g, pc, rhs_l, Dd);
         if (valid) {
-            st_store(Anxt + e, st.g.hi);
-            st_store(Anxt + S + e, st.g.lo);
+            if constexpr (!RG::kCounter) {
+                st_store(Anxt + e, st.g.hi);
+                st_store(Anxt + S + e, st.g.lo);
+            }
 #pragma unroll
             for (int q = 0; q < RL; q++) st_store(Anxt + (2 + q) * S + e, (uint64_t)(int64_t)Dd[q]);
         }
@@ -868,7 +894,7 @@ struct NetRoll {
     }
 };
 
-template <class G>
+template <class G, class RG = Pcg>
 __global__ void __launch_bounds__(2 * WAVE)
 net_roll_kernel(NetParams P, int t_start, StepIO<float, float> io) {
     using R = NetRoll<G>;
@@ -901,13 +927,14 @@ net_roll_kernel(NetParams P, int t_start, StepIO<float, float> io) {
 #pragma unroll
             for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
         }
-        Pcg g = P.cm.rng.load(el);
+        RG g;
+        P.cm.rng.load(el, g);
 #pragma unroll
         for (int r = 0; r < RL; r++)
 #pragma unroll
             for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
         wave_lds_sync();
-        net_demand_loop<G, CH, R::RD>(g, pc, rhs_l, dbuf, lane, K, nch, t_start, P.T);   // barriers 0 .. nch - 1
+        net_demand_loop<G, CH, R::RD>(g, pc, rhs_l, dbuf, lane, K, nch, t_start, P.T, P.cm.ph_step);   // barriers 0 .. nch - 1
         if (valid) P.cm.rng.store_state(e, g);
         return;
     }
@@ -1086,7 +1113,7 @@ struct NetRoll3 {
 // agent's fixed order instead of loading actions, every output is optional,
 // and the evaluate_agent sums accumulate in registers (spec_core, as
 // net_spec_kernel).
-template <class G, int CH_, bool POL>
+template <class G, int CH_, bool POL, class RG = Pcg>
 __global__ void __launch_bounds__(3 * WAVE)
 net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     using R3 = NetRoll3<G, CH_>;
@@ -1125,7 +1152,8 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO po
 #pragma unroll
             for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
         }
-        Pcg g = P.cm.rng.load(el);
+        RG g;
+        P.cm.rng.load(el, g);
 #pragma unroll
         for (int r = 0; r < RL; r++)
 #pragma unroll
@@ -1133,7 +1161,7 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO po
         wave_lds_sync();
         // flat draw loop (stream_flat_loop): up to RD chunks ahead of the dynamics;
         // barriers 0 .. nch - 1 (demand chunk c ready), nch (the obs wave's last chunk)
-        net_demand_loop<G, CH, RD>(g, pc, rhs_l, dbuf, lane, K, nch + 1, t_start, P.T);
+        net_demand_loop<G, CH, RD>(g, pc, rhs_l, dbuf, lane, K, nch + 1, t_start, P.T, P.cm.ph_step);
         if (valid) P.cm.rng.store_state(e, g);
         return;
     }
@@ -1415,17 +1443,24 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
     const dim3 grid((unsigned)((p.cm.N + EPW - 1) / EPW)), block(WAVE);
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
-    const bool ph = p.cm.philox != 0;       // fast stream: net_spec_kernel only (no lookahead, no demand waves)
-    if (!ph && p.ahead && net_ahead_enabled() && !pol && io.K == 1 && t_u >= 0 && t_u < p.T && io.obs &&
+    // fast stream: the split step kernel with a demand-only lookahead, the
+    // rollout kernels with counter-positioned draws, net_spec_kernel otherwise
+    const bool ph = p.cm.philox != 0;
+    if (p.ahead && net_ahead_enabled() && !pol && io.K == 1 && t_u >= 0 && t_u < p.T && io.obs &&
         !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.T)) {
         const bool hit = ahead;
         const int gla = hit ? (int)((p.cm.N + WAVE - 1) / WAVE) : 0;
         const dim3 grid2(grid.x + gla);
-        if (net_split_enabled()) {
+        if (net_split_enabled() || ph) {
             const int gl2 = hit ? (int)((p.cm.N + 2 * WAVE - 1) / (2 * WAVE)) : 0;
             const dim3 g2(grid.x + gl2), b2(2 * WAVE);
-            if (hit) hipLaunchKernelGGL((net_step2_kernel<G, true>), g2, b2, lds, s, p, t_u, io, slot, gl2);
-            else hipLaunchKernelGGL((net_step2_kernel<G, false>), g2, b2, lds, s, p, t_u, io, slot, gl2);
+            if (ph) {
+                if (hit) hipLaunchKernelGGL((net_step2_kernel<G, true, PhiloxGen>), g2, b2, lds, s, p, t_u, io, slot, gl2);
+                else hipLaunchKernelGGL((net_step2_kernel<G, false, PhiloxGen>), g2, b2, lds, s, p, t_u, io, slot, gl2);
+            } else {
+                if (hit) hipLaunchKernelGGL((net_step2_kernel<G, true>), g2, b2, lds, s, p, t_u, io, slot, gl2);
+                else hipLaunchKernelGGL((net_step2_kernel<G, false>), g2, b2, lds, s, p, t_u, io, slot, gl2);
+            }
         } else {
             if (hit) hipLaunchKernelGGL((net_step1_kernel<G, true>), grid2, block, lds, s, p, t_u, io, slot, gla);
             else hipLaunchKernelGGL((net_step1_kernel<G, false>), grid2, block, lds, s, p, t_u, io, slot, gla);
@@ -1436,7 +1471,9 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
     }
     // the other kernels draw from cm.rng: commit the cache first (the lock-step
     // NEXT_STEP autoreset launch draws nothing and keeps it)
-    if (ahead && !(!pol && io.K == 1 && t_u >= p.T)) {
+    if (ph) {
+        ahead = false;   // the fast stream's cache (demands only) is for a counter value now passed
+    } else if (ahead && !(!pol && io.K == 1 && t_u >= p.T)) {
         const hipError_t ce = net_commit_launch(p, slot, s);
         ahead = false;
         if (ce != hipSuccess) return ce;
@@ -1448,19 +1485,19 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
     } while (0)
     // ... and the in-kernel ConstantOrder agent on the 3-role kernel
     const bool pol_roll = pol && pol->kind == POL_CONSTANT && net_pol_roll_enabled();
-    if (!ph && (!pol || pol_roll) && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
+    if ((!pol || pol_roll) && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
         (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
         const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE));
         using R3 = NetRoll3<G, NET_ROLL3_CH>;
-        if (pol) {
-            hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, true>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv);
-            return hipGetLastError();
-        }
-        if (net_roll3_use(p.cm.N)) {
-            hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, false>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv);
-        } else {
-            hipLaunchKernelGGL((net_roll_kernel<G>), gr, dim3(2 * WAVE), NetRoll<G>::lds(), s, p, t_u, io);
-        }
+#define RK_(RG)                                                                                                       \
+    do {                                                                                                              \
+        if (pol) hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, true, RG>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv); \
+        else if (net_roll3_use(p.cm.N)) hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, false, RG>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv); \
+        else hipLaunchKernelGGL((net_roll_kernel<G, RG>), gr, dim3(2 * WAVE), NetRoll<G>::lds(), s, p, t_u, io);    \
+    } while (0)
+        if (ph) RK_(PhiloxGen);
+        else RK_(Pcg);
+#undef RK_
         return hipGetLastError();
     }
     if (pol) {

@@ -239,3 +239,42 @@ def test_fast_stream_lookahead_across_switches_and_checkpoints(gpu, monkeypatch)
     for i, (x, y) in enumerate(zip(a, b)):
         assert torch.equal(x.view(torch.uint8) if x.dtype == torch.float64 else x,
                            y.view(torch.uint8) if y.dtype == torch.float64 else y), i
+
+
+def _net_fast_run(gpu, graph, n, fused, monkeypatch):
+    import invsim
+    from invsim.topology import custom_graph, default_graph
+    for v in ("INVSIM_NET_AHEAD", "INVSIM_NET_ROLL", "INVSIM_NET_POL_ROLL"):
+        monkeypatch.setenv(v, "1" if fused else "0")
+    monkeypatch.setenv("INVSIM_NET_ROLL3", "0" if n == 40000 else "1")   # 40 000: the 2-role net_roll_kernel
+    g = default_graph() if graph == "default" else custom_graph()
+    env = invsim.NetInvMgmtBacklogEnv(n, device=gpu, graph=g, demand_stream="philox", record_demand=True)
+    env.reset(seed=19)
+    gen = torch.Generator(device=gpu)
+    gen.manual_seed(6)
+    A = env.action_dim
+    out = []
+    for k in range(33):                                   # split steps with the demand-only lookahead
+        a = torch.rand((n, A), device=gpu, generator=gen) * 60
+        o, r, te, tr, info = env.step(a)
+        out += [o.clone(), r.clone(), tr.clone(), info["demand"].clone()]
+    acts = torch.rand((45, n, A), device=gpu, generator=gen) * 60
+    out += list(env.rollout(acts))                         # 3-role / 2-role rollout kernels
+    m = torch.zeros((n, invsim.policies.metrics_dim(env)), dtype=torch.float64, device=gpu)
+    pol = env.rollout_policy(invsim.ConstantOrderAgent(0.1), 40, obs=True, actions=True, metrics=m)
+    out += [pol[k] for k in sorted(pol)] + [m]
+    out.append(env.get_state())
+    return out
+
+
+@pytest.mark.parametrize("graph,n", [("default", 4096), ("default", 40000), ("custom", 5000)])
+def test_fast_stream_net_fused_kernels_equal_spec_kernel(gpu, monkeypatch, graph, n):
+    """Net: the fast stream on net_step2_kernel (demand-only lookahead) and the
+    rollout kernels (3-role; 2-role for the 40 000-env case) == net_spec_kernel,
+    bit for bit."""
+    a = _net_fast_run(gpu, graph, n, True, monkeypatch)
+    b = _net_fast_run(gpu, graph, n, False, monkeypatch)
+    assert len(a) == len(b)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x.view(torch.uint8) if x.dtype == torch.float64 else x,
+                           y.view(torch.uint8) if y.dtype == torch.float64 else y), i

@@ -5,7 +5,7 @@ O=gpurun_out/fast_ab
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_fast_stream.py -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-for w in ${WLS:-invmgmt_backlog invmgmt_lostsales}; do
+for w in ${WLS:-invmgmt_backlog invmgmt_lostsales net_backlog}; do
   for ds in numpy philox; do
     for m in step policy; do
       timeout -k 10 120 python bench.py --workload $w --demand-stream $ds --mode $m --no-cpu-baseline > $O/${w}_${ds}_${m}.json 2> $O/${w}_${ds}_${m}.err || { tail -20 $O/${w}_${ds}_${m}.err; exit 1; }
