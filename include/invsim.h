@@ -48,7 +48,8 @@
 extern "C" {
 #endif
 
-#define INVSIM_ABI_VERSION 2   /* 2: market samplers appended to invsim_netinvmgmt_spec */
+#define INVSIM_ABI_VERSION 3   /* 2: market samplers appended to invsim_netinvmgmt_spec
+                                  3: graph capture (invsim_capture_begin / _end, invsim_position) */
 
 #define INVSIM_OK 0
 #define INVSIM_EINVAL (-22)
@@ -314,6 +315,35 @@ int invsim_state_field(const invsim_handle *h, int32_t idx, char name[32], int64
                        int32_t *elem_bytes, int32_t *rows, int64_t *row_stride);
 int invsim_get_state(invsim_handle *h, void *dst, void *stream);
 int invsim_set_state(invsim_handle *h, const void *src, void *stream);
+
+/* HIP-graph capture of a step loop (SURVEY §7 layer 5; the reference's
+ * per-step loop is the caller's `for t: a = agent(obs); env.step(a)`,
+ * benchmark_InvManagementBacklogEnv.py:389-440).  The caller records its own
+ * stream capture (hipStreamBeginCapture ... hipStreamEndCapture, or
+ * torch.cuda.graph) of any mix of its policy launches and invsim_reset /
+ * invsim_step / invsim_rollout / invsim_rollout_policy calls on one handle,
+ * bracketed by invsim_capture_begin / invsim_capture_end.  Inside the bracket
+ * those calls enqueue kernels only; a call that would need a host
+ * synchronisation (autoreset DISABLED after a masked reset, get/set_state,
+ * status, set_demand_stream) or the fast demand stream (its launch-step
+ * counter is a launch parameter and would repeat on replay) fails with
+ * INVSIM_EINVAL.  A step call on a capturing stream outside the bracket fails
+ * too (the handle's host-side position would drift from the device).
+ *
+ * The host side of a handle keeps a position (lock-step period, demand
+ * lookahead slot) that picks each launch's kernel and parameters.  Nothing
+ * runs during capture, so capture_end puts the position back to where
+ * capture_begin found it and returns INVSIM_OK only if the captured calls
+ * bring it back there (a whole number of episode cycles: periods + 1 steps
+ * with NEXT_STEP autoreset, periods with SAME_STEP), so that every replay
+ * starts where the graph was recorded; otherwise INVSIM_ERANGE (the graph
+ * must not be replayed).  *steps receives the env steps captured.
+ * invsim_position returns an opaque token of that position: a graph replays
+ * correctly whenever the token equals its value at capture_begin (it does
+ * after any number of replays, and after eager calls that close a cycle). */
+int invsim_capture_begin(invsim_handle *h);
+int invsim_capture_end(invsim_handle *h, int64_t *steps);
+int invsim_position(const invsim_handle *h, int64_t *pos);
 
 #ifdef __cplusplus
 }

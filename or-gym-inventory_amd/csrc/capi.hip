@@ -72,6 +72,13 @@ struct invsim_handle {
     uint64_t ph_step = 0;
     int64_t o_phstep = 0;
     bool ph_from_blob = false;  // set_state loaded the blob: its philox_step is the counter
+    // graph capture (invsim_capture_begin / _end): the host-side position at
+    // begin, put back at end, and the env steps the captured calls enqueue
+    bool capturing = false;
+    bool cap_t_known = true, cap_la_valid = false;
+    int32_t cap_t_cur = 0;
+    int cap_la_slot = 0;
+    int64_t cap_steps = 0;
     std::string err;
 };
 
@@ -129,6 +136,28 @@ int fail(invsim_handle *h, int code, const std::string &msg) {
 
 int hip_fail(invsim_handle *h, hipError_t e, const char *what) {
     return fail(h, INVSIM_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Calls that synchronise with the host cannot be recorded into a graph.
+int refuse_in_capture(invsim_handle *h, const char *what) {
+    if (!h->capturing) return INVSIM_OK;
+    return fail(h, INVSIM_EINVAL, std::string(what) + " synchronises with the host and cannot be captured "
+                                                      "(between invsim_capture_begin and invsim_capture_end)");
+}
+
+// A launching call on a stream that is being captured must be inside the
+// capture bracket: otherwise the host-side position advances while the device
+// state does not (nothing runs until the graph is replayed).
+int capture_check(invsim_handle *h, hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+        (void)hipGetLastError();   // e.g. the legacy stream while another one captures: not ours to record
+        st = hipStreamCaptureStatusNone;
+    }
+    if (st == hipStreamCaptureStatusActive && !h->capturing)
+        return fail(h, INVSIM_EINVAL, "this stream is being captured into a graph: bracket the capture with "
+                                      "invsim_capture_begin / invsim_capture_end");
+    return INVSIM_OK;
 }
 
 // Lay out named SoA fields (rows x Npad elements each, 256-byte aligned).
@@ -707,6 +736,7 @@ static int ph_counter_sync(invsim_handle *h, hipStream_t s) {
 
 int invsim_set_autoreset(invsim_handle *h, int32_t mode) {
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (int rc = refuse_in_capture(h, "set_autoreset")) return rc;
     if (!valid_autoreset(mode)) return fail(h, INVSIM_EINVAL, "bad autoreset mode");
     h->cm.autoreset = mode;
     sync_common(h);
@@ -728,6 +758,7 @@ int invsim_info_record_dim(const invsim_handle *h, int32_t *dim) {
 
 int invsim_set_info_record(invsim_handle *h, void *record) {
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (int rc = refuse_in_capture(h, "set_info_record")) return rc;
     if (record && info_record_dim(h) == 0) return fail(h, INVSIM_EINVAL, "this env family has no step record");
     h->cm.info_rec = record;
     sync_common(h);
@@ -736,6 +767,7 @@ int invsim_set_info_record(invsim_handle *h, void *record) {
 
 int invsim_set_info_demand(invsim_handle *h, int64_t *demand) {
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (int rc = refuse_in_capture(h, "set_info_demand")) return rc;
     h->cm.info_demand = demand;
     sync_common(h);
     return INVSIM_OK;
@@ -757,6 +789,7 @@ int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int6
     TraceRange tr_("invsim_seed_range");
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
     if (first < 0) return fail(h, INVSIM_EINVAL, "first_index must be >= 0");
+    if (int rc = capture_check(h, (hipStream_t)stream)) return rc;
     DeviceGuard g(h->device);
     int rc = commit_rng(h, (hipStream_t)stream);   // a masked seed keeps the other streams
     if (rc != INVSIM_OK) return rc;
@@ -769,6 +802,7 @@ int invsim_seed_words(invsim_handle *h, const uint32_t *words, const int32_t *nw
                       const uint8_t *mask, void *stream) {
     TraceRange tr_("invsim_seed_words");
     if (!h || (!words && h->N) || (!nwords && h->N)) return fail(h, INVSIM_EINVAL, "null argument");
+    if (int rc = capture_check(h, (hipStream_t)stream)) return rc;
     DeviceGuard g(h->device);
     int rc = commit_rng(h, (hipStream_t)stream);
     if (rc != INVSIM_OK) return rc;
@@ -787,6 +821,9 @@ static int materialize_period(invsim_handle *h, hipStream_t s) {
 int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream) {
     TraceRange tr_("invsim_reset");
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (int rc = capture_check(h, (hipStream_t)stream)) return rc;
+    if (h->capturing && h->demand_stream == INVSIM_DEMAND_PHILOX)
+        return fail(h, INVSIM_EINVAL, "graph capture needs the numpy demand stream");
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
     if (mask) {
@@ -823,6 +860,16 @@ int invsim_reset(invsim_handle *h, const uint8_t *mask, void *obs, void *stream)
 static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, double *reward,
                      uint8_t *terminated, uint8_t *truncated, void *final_obs, hipStream_t s,
                      const PolicyIO *pol = nullptr) {
+    if (int rc = capture_check(h, s)) return rc;
+    if (h->capturing) {
+        if (h->demand_stream == INVSIM_DEMAND_PHILOX)
+            return fail(h, INVSIM_EINVAL, "graph capture needs the numpy demand stream: the fast stream's launch-step "
+                                          "counter is a launch parameter and would repeat on every replay");
+        if (!h->t_known && h->cm.autoreset == AR_DISABLED && !h->past_ok)
+            return fail(h, INVSIM_EINVAL, "graph capture of steps with autoreset DISABLED after a masked reset: "
+                                          "the horizon check reads the device status word (a host synchronisation)");
+        h->cap_steps += K;
+    }
     int t_u = -1;
     if (h->t_known) {
         t_u = h->t_cur;
@@ -1014,6 +1061,7 @@ int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear) {
 int invsim_set_demand_stream(invsim_handle *h, int32_t mode) {
     TraceRange tr_("invsim_set_demand_stream");
     if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (int rc = refuse_in_capture(h, "set_demand_stream")) return rc;
     if (mode != INVSIM_DEMAND_NUMPY && mode != INVSIM_DEMAND_PHILOX)
         return fail(h, INVSIM_EINVAL, "demand stream must be INVSIM_DEMAND_NUMPY or INVSIM_DEMAND_PHILOX");
     if (mode == h->demand_stream) return INVSIM_OK;
@@ -1043,6 +1091,7 @@ int invsim_kernel_variant(const invsim_handle *h, int32_t *variant) {
 
 int invsim_status(invsim_handle *h, uint32_t *flags, int32_t clear) {
     if (!h || !flags) return fail(h, INVSIM_EINVAL, "null argument");
+    if (int rc = refuse_in_capture(h, "status")) return rc;
     DeviceGuard g(h->device);
     hipError_t e = hipMemcpy(flags, h->cm.status, sizeof(uint32_t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(h, e, "status read");
@@ -1079,6 +1128,7 @@ int invsim_state_field(const invsim_handle *h, int32_t idx, char name[32], int64
 int invsim_get_state(invsim_handle *h, void *dst, void *stream) {
     TraceRange tr_("invsim_get_state");
     if (!h || !dst) return fail(h, INVSIM_EINVAL, "null argument");
+    if (int rc = refuse_in_capture(h, "get_state")) return rc;
     DeviceGuard g(h->device);
     int rc = materialize_period(h, (hipStream_t)stream);  // the blob carries per-env periods
     if (rc == INVSIM_OK) rc = commit_rng(h, (hipStream_t)stream);   // and the committed PCG64 states
@@ -1097,6 +1147,7 @@ int invsim_get_state(invsim_handle *h, void *dst, void *stream) {
 int invsim_set_state(invsim_handle *h, const void *src, void *stream) {
     TraceRange tr_("invsim_set_state");
     if (!h || !src) return fail(h, INVSIM_EINVAL, "null argument");
+    if (int rc = refuse_in_capture(h, "set_state")) return rc;
     DeviceGuard g(h->device);
     hipError_t e = hipMemcpyAsync(h->arena, src, (size_t)h->arena_bytes, hipMemcpyDeviceToDevice,
                                   (hipStream_t)stream);
@@ -1104,6 +1155,54 @@ int invsim_set_state(invsim_handle *h, const void *src, void *stream) {
     h->t_known = false;  // periods now come from the blob
     h->la_valid = false;
     h->ph_from_blob = true;   // and the fast stream's counter (read when next needed)
+    return INVSIM_OK;
+}
+
+// ------------------------------------------------------------------ graph capture
+int invsim_capture_begin(invsim_handle *h) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (h->capturing) return fail(h, INVSIM_EINVAL, "capture_begin: this handle is already capturing");
+    if (h->demand_stream == INVSIM_DEMAND_PHILOX)
+        return fail(h, INVSIM_EINVAL, "graph capture needs the numpy demand stream: the fast stream's launch-step "
+                                      "counter is a launch parameter and would repeat on every replay");
+    h->capturing = true;
+    h->cap_t_known = h->t_known;
+    h->cap_t_cur = h->t_cur;
+    h->cap_la_valid = h->la_valid;
+    h->cap_la_slot = h->la_slot;
+    h->cap_steps = 0;
+    return INVSIM_OK;
+}
+
+int invsim_capture_end(invsim_handle *h, int64_t *steps) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (!h->capturing) return fail(h, INVSIM_EINVAL, "capture_end without capture_begin");
+    if (steps) *steps = h->cap_steps;
+    const bool closed = h->t_known == h->cap_t_known && (!h->t_known || h->t_cur == h->cap_t_cur) &&
+                        h->la_valid == h->cap_la_valid && (!h->la_valid || h->la_slot == h->cap_la_slot);
+    const int32_t t_end = h->t_known ? h->t_cur : -1;
+    const bool la_end = h->la_valid;
+    // nothing ran: the device is still where capture_begin found it
+    h->capturing = false;
+    h->t_known = h->cap_t_known;
+    h->t_cur = h->cap_t_cur;
+    h->la_valid = h->cap_la_valid;
+    h->la_slot = h->cap_la_slot;
+    if (closed) return INVSIM_OK;
+    std::string msg = "the captured calls (" + std::to_string(h->cap_steps) + " env steps) move the handle from period " +
+                      std::to_string(h->t_known ? h->t_cur : -1) + " to " + std::to_string(t_end);
+    if (la_end != h->la_valid) msg += " and change the demand lookahead state";
+    msg += ": a replay would not start where the graph was recorded; capture a whole number of episode cycles (" +
+           std::to_string(h->horizon + (h->cm.autoreset == AR_NEXT_STEP ? 1 : 0)) +
+           " steps) from a handle that has already stepped once";
+    return fail(h, INVSIM_ERANGE, msg);
+}
+
+int invsim_position(const invsim_handle *h, int64_t *pos) {
+    if (!h || !pos) return fail(nullptr, INVSIM_EINVAL, "null argument");
+    const uint64_t t = h->t_known ? (uint32_t)h->t_cur : 0xFFFFFFFFu;
+    const uint64_t la = h->la_valid ? 2u + (uint64_t)(h->la_slot & 1) : 0u;
+    *pos = (int64_t)(t | (la << 32) | ((uint64_t)(h->demand_stream & 1) << 34));
     return INVSIM_OK;
 }
 

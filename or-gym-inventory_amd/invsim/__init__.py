@@ -28,11 +28,12 @@ _LAZY = {
     "sSPolicyAgent": "policies",
     "evaluate_agent": "policies",
     "rollout_policy": "policies",
+    "StepGraph": "graphs",
 }
 
 
 _SUBMODULES = ("policies", "topology", "distributed", "spaces", "vector", "newsvendor",
-               "inventory_management", "network_management")
+               "inventory_management", "network_management", "graphs")
 
 
 def __getattr__(name):

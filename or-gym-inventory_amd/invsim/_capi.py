@@ -27,7 +27,9 @@ EXPORTS = (
     "invsim_state_bytes",
     "invsim_state_field", "invsim_get_state", "invsim_set_state", "invsim_episode_fold",
     "invsim_debug_ptrs_stats", "invsim_set_demand_stream", "invsim_demand_stream",
+    "invsim_capture_begin", "invsim_capture_end", "invsim_position",
 )
+ABI_VERSION = 3
 DEMAND_STREAMS = {"numpy": 0, "philox": 1}
 
 
@@ -106,6 +108,9 @@ def _declare(lib):
         "invsim_debug_ptrs_stats": ([P, I32], C.c_int),
         "invsim_set_demand_stream": ([H, I32], C.c_int),
         "invsim_demand_stream": ([H, P], C.c_int),
+        "invsim_capture_begin": ([H], C.c_int),
+        "invsim_capture_end": ([H, P], C.c_int),
+        "invsim_position": ([H, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

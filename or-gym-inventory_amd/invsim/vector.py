@@ -310,6 +310,19 @@ class InvSimVectorEnv:
         _capi.check(self._lib.invsim_kernel_variant(self._h, _capi.C.byref(v)), self._h, "kernel_variant")
         return v.value
 
+    def position(self):
+        """Opaque token of the host-side position (lock-step period, lookahead
+        slot) that picks each launch's kernel; see invsim.graphs."""
+        p = _capi.C.c_int64()
+        _capi.check(self._lib.invsim_position(self._h, _capi.C.byref(p)), self._h, "position")
+        return p.value
+
+    def capture(self, fn, warmup=1, pool=None):
+        """Record fn() (a policy's torch ops + calls on this env) as one HIP
+        graph: returns an invsim.graphs.StepGraph whose replay() reruns it."""
+        from .graphs import StepGraph
+        return StepGraph(self, fn, warmup=warmup, pool=pool)
+
     # -- state -----------------------------------------------------------------
     def state_bytes(self):
         b = _capi.C.c_int64()
