@@ -34,6 +34,7 @@ namespace invsim {
 int net_spec_match(const invsim_netinvmgmt_spec &h);   // netspec.hip
 #ifdef INVSIM_PTRS_STATS
 hipError_t ptrs_stats_nv(unsigned long long *out, bool clear);
+hipError_t ptrs_stats_nv_ph(unsigned long long *out, bool clear);
 hipError_t ptrs_stats_im(unsigned long long *out, bool clear);
 hipError_t ptrs_stats_im_ph(unsigned long long *out, bool clear);
 hipError_t ptrs_stats_netspec(unsigned long long *out, bool clear);
@@ -1037,8 +1038,8 @@ int invsim_episode_fold(const double *reward, const uint8_t *terminated, const u
 int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear) {
     if (!out) return fail(nullptr, INVSIM_EINVAL, "null argument");
 #ifdef INVSIM_PTRS_STATS
-    hipError_t (*tus[5])(unsigned long long *, bool) = {ptrs_stats_nv, ptrs_stats_im, ptrs_stats_im_ph,
-                                                        ptrs_stats_netspec, ptrs_stats_net};
+    hipError_t (*tus[6])(unsigned long long *, bool) = {ptrs_stats_nv, ptrs_stats_nv_ph, ptrs_stats_im,
+                                                        ptrs_stats_im_ph, ptrs_stats_netspec, ptrs_stats_net};
     out[0] = out[1] = out[3] = 0;
     out[2] = 0x7ff0000000000000ull;
     for (auto f : tus) {

@@ -368,6 +368,9 @@ hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, h
 hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
                          bool &ahead, int &slot, hipStream_t s);
 hipError_t nv_commit_launch(const NvParams &p, int slot, hipStream_t s);
+// the fast-stream (cm.philox) kernels, newsvendor_ph.hip (demand-only lookahead cache)
+hipError_t nv_run_launch_ph(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
+                            bool &ahead, int &slot, hipStream_t s);
 
 hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_t *mask,
                            int64_t *obs, hipStream_t s);

@@ -529,7 +529,8 @@ __device__ __forceinline__ PtrsConst nv_rate_const(double lam) {
 }
 
 // np_poisson_dyn with the episode's constants (same draws, same arithmetic)
-__device__ __forceinline__ int64_t nv_poisson_c(Pcg &g, const PtrsConst &c, const double *lgtab) {
+template <class G>
+__device__ __forceinline__ int64_t nv_poisson_c(G &g, const PtrsConst &c, const double *lgtab) {
     if (c.lam >= 10) return np_poisson_ptrs_lg(g, c, lgtab, RHS_LDS_MAX);
     if (c.lam == 0) return 0;
     return np_poisson_mult(g, c.enlam);
@@ -552,7 +553,11 @@ __device__ __forceinline__ int64_t nv_poisson_c(Pcg &g, const PtrsConst &c, cons
 // cur, the host flips the slots, and cm.rng is brought up to date from it
 // (nv_commit_kernel) only before something reads it.  Streams are consumed in
 // the reference's order; arithmetic as nv_step_regs (newsvendor.py:125-204).
-template <int LT, bool HIT, bool PRODUCE>
+// RG = PhiloxGen (the fast stream, newsvendor_ph.hip): the same lookahead, but a
+// draw is a function of (key, launch step, mu) only, so a slot holds just the
+// next step's demand (row 2) and no generator state is read or written; with
+// !PRODUCE the host launches no lookahead workgroups (there is nothing to commit).
+template <int LT, bool HIT, bool PRODUCE, class RG = Pcg>
 __global__ void __launch_bounds__(WAVE)
 nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
     extern __shared__ __attribute__((aligned(16))) float nv_tile[];
@@ -574,6 +579,37 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
         const int64_t e = (int64_t)(PRODUCE ? bid >> 1 : bid) * WAVE + lane;
         const bool valid = e < N;
         const int64_t el = valid ? e : N - 1;
+        if constexpr (RG::kCounter) {   // the fast stream: the draw of launch step ph_step + 1
+            if (!PRODUCE) return;
+            RG g;
+            P.cm.rng.load(el, g);
+            g.set_step(P.cm.ph_step + 1);
+            g.sub(0);
+            const double mu = P.par[4 * S + el];
+            const bool mult_wg = bid & 1;
+            if (!mult_wg) {
+                TableStage ts;
+                ts.dst = lg_l;
+                ts.load(P.lgtab, RHS_LDS_MAX, lane);
+                ts.flush(lane);
+            }
+            const bool mine = mult_wg == (mu < 10 && mu != 0);
+            if (!mine) return;
+            PtrsConst c;
+            c.lam = mu;
+            c.a = P.pcon[el];
+            c.b = P.pcon[S + el];
+            c.vr = P.pcon[2 * S + el];
+            c.loglam = P.pcon[3 * S + el];
+            c.log_invalpha = P.pcon[4 * S + el];
+            c.enlam = P.pcon[5 * S + el];
+            c.a2 = 2 * c.a;
+            c.k0 = 0;
+            c.nk = 0;
+            const int64_t dn = nv_poisson_c(g, c, lg_l);
+            if (valid) st_store(Anxt + 2 * S + e, (uint64_t)dn);
+            return;
+        } else {
         Pcg g;
         g.hi = Acur[el];
         g.lo = Acur[S + el];
@@ -647,6 +683,7 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
         TWAIT();
         TPROBE(5);
         return;
+        }
     }
     const int64_t e0 = (int64_t)(bid - (HIT ? gla : 0)) * EPW;
     const int64_t e = e0 + lane;
@@ -655,13 +692,15 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
     const int64_t el = valid ? e : N - 1;
     float *trow = nv_tile + (int64_t)lane * O;
     constexpr int TILE_IT = (EPW * 21 * 4 + 16 * WAVE - 1) / (16 * WAVE);
-    NvState<LT> st;
+    NvState<LT, RG> st;
     TableStage ts;
     int64_t dpre = -1;
     if (HIT) {
         dpre = (int64_t)Acur[2 * S + el];
     } else {
-        st.g = P.cm.rng.load(el);
+        P.cm.rng.load(el, st.g);
+        st.g.set_step(P.cm.ph_step);
+        st.g.sub(0);
         ts.dst = lg_l;
         ts.load(P.lgtab, RHS_LDS_MAX, lane);
     }
@@ -705,14 +744,19 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
     store_tile<TILE_IT>(nv_tile, io.obs + e0 * O, (int64_t)nvalid * O, lane);
     TPROBE(4);
     if (!HIT) {   // PRODUCE (the host runs nv_run_kernel for !HIT && !PRODUCE)
-        if (valid) {
+        if constexpr (RG::kCounter) {
+            st.g.set_step(P.cm.ph_step + 1);
+            st.g.sub(0);
+        } else if (valid) {
             st_store((uint64_t *)Acur + e, st.g.hi);
             st_store((uint64_t *)Acur + S + e, st.g.lo);
         }
         const int64_t dn = nv_poisson_c(st.g, c, lg_l);
         if (valid) {
-            st_store(Anxt + e, st.g.hi);
-            st_store(Anxt + S + e, st.g.lo);
+            if constexpr (!RG::kCounter) {
+                st_store(Anxt + e, st.g.hi);
+                st_store(Anxt + S + e, st.g.lo);
+            }
             st_store(Anxt + 2 * S + e, (uint64_t)dn);
         }
     }
@@ -890,14 +934,134 @@ struct NvRoll {
     static constexpr size_t lds() {
         return tile_bytes() + RHS_LDS_MAX * sizeof(double) + 2 * (size_t)CH * WAVE * sizeof(int64_t) +
                2 * NP * (size_t)WAVE * sizeof(double) + (size_t)WAVE * sizeof(double) +
-               4 * (JUMP_MAX + 1) * sizeof(uint64_t);
+               4 * (JUMP_MAX + 1) * sizeof(uint64_t) + 2 * 2 * (size_t)WAVE * sizeof(uint64_t);
     }
 };
+
+// The two stream waves of nv_roll_kernel on the fast stream.  A draw is a
+// function of (key, launch step, mu) only -- no generator state, no order
+// between draws -- so the waves split the chunk's draws instead of the sampler
+// branches: wave `role` draws launch steps j = role, role + 2, ... of its
+// lane's env when that env is on numpy's PTRS branch (one Philox block per
+// candidate: U and V are its two 53-bit halves, as PhiloxGen hands them out),
+// and the chunk's multiplication-branch draws (0 < mu < 10: few envs) are
+// spread over both waves' lanes as (env, step) tasks.  The reset (5 uniforms
+// of the reset step's own counter block, :100-123) is wave 0's; its params go
+// to the other waves through the reset handoff rows of pbuf.  Same draws as
+// nv_run_kernel<..., PhiloxGen> (test_fast_stream_newsvendor_fused_kernels_...).
+template <int LT>
+__device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int lane, int64_t e, int64_t el, bool valid,
+                                             int t_start, int K, bool nxt, double *lg_l, int64_t *dbuf,
+                                             double *pbuf, uint64_t *kb) {
+    constexpr int CH = NvRoll<LT>::CH, NP = NvRoll<LT>::NP;
+    const int64_t S = P.cm.Npad;
+    {   // both waves draw PTRS candidates: each writes the whole (identical) table
+        TableStage ts;
+        ts.dst = lg_l;
+        ts.load(P.lgtab, RHS_LDS_MAX, lane);
+        ts.flush(lane);
+    }
+    NvState<LT, PhiloxGen> st;
+    P.cm.rng.load(el, st.g);
+    const uint2 key = st.g.key;
+    PtrsConst c = nv_rate_const(P.par[4 * S + el]);
+    uint64_t *kw = kb + role * 2 * WAVE;   // this wave's task table: keys [WAVE], exp(-mu) bits [WAVE]
+    bool reset_any = false;
+    int t = t_start, cb = 0;
+    for (int k0 = 0; k0 < K;) {
+        int len;
+        bool rs;
+        nv_chunk(t, K - k0, P.step_limit, nxt, NvRoll<LT>::CH, len, rs);
+        const int nd = len - (rs ? 1 : 0);                   // the reset step draws none
+        int64_t *dcol = dbuf + cb * CH * WAVE;
+        const uint64_t ph0 = P.cm.ph_step + (uint64_t)k0;    // launch step of the chunk's first step
+#if defined(INVSIM_ABL_ROLL_NO_DRAW)
+        for (int j = role; j < nd; j += 2) dcol[j * WAVE + lane] = 20;
+#else
+        if (c.lam >= 10) {   // numpy random_poisson_ptrs, one candidate per iteration, lanes independent
+            uint32_t cj = 0;                                  // candidate = counter block of the draw
+            for (int j = role; j < nd;) {
+                const uint64_t stp = ph0 + (uint64_t)j;
+                PhiloxBlock b;
+                const uint4 x = b.block(make_uint4(cj, 0u, (uint32_t)stp, (uint32_t)(stp >> 32)), key);
+                const double U = (double)((((uint64_t)x.y << 32) | x.x) >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+                const double V = (double)((((uint64_t)x.w << 32) | x.z) >> 11) * (1.0 / 9007199254740992.0);
+                const double us = 0.5 - fabs(U);
+                const int64_t kd = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+                bool acc = (us >= 0.07) && (V <= c.vr);
+                if (!acc && !((kd < 0) || ((us < 0.013) && (V > us)))) {
+                    const double r = (kd < RHS_LDS_MAX)
+                                         ? (-c.lam + (double)kd * c.loglam) - lg_l[kd < RHS_LDS_MAX ? kd : 0]
+                                         : -c.lam + (double)kd * c.loglam - np_loggam((double)(kd + 1));
+                    acc = ptrs_log_accept(c, V, us, r);
+                }
+                if (acc) {
+                    dcol[j * WAVE + lane] = kd;
+                    j += 2;
+                    cj = 0;
+                } else {
+                    cj++;
+                }
+            }
+        } else if (c.lam == 0) {
+            for (int j = role; j < nd; j += 2) dcol[j * WAVE + lane] = 0;
+        }
+        {   // numpy random_poisson_mult (0 < mu < 10, or NaN): task q = (env rank q / nd, step q % nd)
+            const uint64_t mm = (uint64_t)__ballot(nv_mult_branch(c.lam) && nd > 0);
+            const int nm = __popcll(mm);
+            if (nm > 0) {
+                kw[lane] = ((uint64_t)key.y << 32) | key.x;
+                kw[WAVE + lane] = (uint64_t)__double_as_longlong(c.enlam);
+                wave_lds_sync();
+                // a divergent loop: keys and rates of other lanes come through LDS
+                for (int q = lane + role * WAVE; q < nm * nd; q += 2 * WAVE) {
+                    const int r = q / nd, j = q - r * nd;
+                    uint64_t m = mm;
+                    for (int i = 0; i < r; i++) m &= m - 1;   // the r-th mult env's lane
+                    const int src = (int)__builtin_ctzll(m);
+                    PhiloxGen g;
+                    const uint64_t kk = kw[src];
+                    g.key = make_uint2((uint32_t)kk, (uint32_t)(kk >> 32));
+                    g.set_step(ph0 + (uint64_t)j);
+                    g.sub(0);
+                    dcol[j * WAVE + src] = np_poisson_mult(g, __longlong_as_double((long long)kw[WAVE + src]));
+                }
+                wave_lds_sync();
+            }
+        }
+#endif
+        double *pb = pbuf + cb * NP * WAVE + lane;
+        if (rs && role == 0) {                                // reset() at launch step k0 + len - 1
+            st.g.set_step(ph0 + (uint64_t)(len - 1));
+            nv_reset_regs<LT>(P, e, st, nullptr, false);
+#pragma unroll
+            for (int j = 0; j < 5; j++) pb[j * WAVE] = st.par[j];
+        }
+        nv_wg_sync();   // barrier: chunk ready
+        if (rs) {
+#pragma unroll
+            for (int j = 0; j < 5; j++) st.par[j] = pb[j * WAVE];
+            c = nv_rate_const(st.par[4]);
+            reset_any = true;
+            t = 0;
+        } else {
+            t += len;
+        }
+        k0 += len;
+        cb ^= 1;
+    }
+    if (valid && reset_any && role == 0) {
+#pragma unroll
+        for (int j = 0; j < 5; j++) P.par[j * S + e] = st.par[j];
+    }
+}
 
 // POL (invsim_rollout_policy): the dynamics wave asks the agent for each
 // step's order (OrderUpTo / ClassicNV / (s, S) / Constant, as nv_run_kernel)
 // instead of loading it; every output optional, the per-env sums in registers.
-template <int LT, bool POL>
+// RG = PhiloxGen (the fast stream, newsvendor_ph.hip): the stream waves run
+// nv_stream_ph instead (above); the dynamics wave is the same.
+template <int LT, bool POL, class RG = Pcg>
 __global__ void __launch_bounds__(3 * WAVE)
 nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     using R = NvRoll<LT>;
@@ -910,6 +1074,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     double *pbuf = reinterpret_cast<double *>(dbuf + 2 * CH * WAVE);      // [2][NP][WAVE]
     double *ubuf = pbuf + 2 * NP * WAVE;                                   // [WAVE] mult wave's uniforms
     uint64_t *jt = reinterpret_cast<uint64_t *>(ubuf + WAVE);              // [4][JUMP_MAX + 1] jump table
+    uint64_t *kb = jt + 4 * (JUMP_MAX + 1);                                // [2][2][WAVE] fast stream: keys, rates
     const int lane = threadIdx.x & (WAVE - 1);
     const int role = threadIdx.x / WAVE;
     const int64_t N = P.cm.N;
@@ -921,7 +1086,12 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
     const int K = io.K;
     const bool nxt = P.cm.autoreset == AR_NEXT_STEP;
-    if (role < 2) {   // ---- stream waves
+    if constexpr (RG::kCounter) {
+        if (role < 2) {   // ---- the fast stream's two stream waves
+            nv_stream_ph<LT>(P, role, lane, e, el, valid, t_start, K, nxt, lg_l, dbuf, pbuf, kb);
+            return;
+        }
+    } else if (role < 2) {   // ---- stream waves
         const bool multw = role == 1;
         TableStage ts;
         if (!multw) {
@@ -1166,14 +1336,6 @@ nv_reset_kernel(NvParams P, const uint8_t *__restrict__ mask, float *__restrict_
 
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
-}  // namespace
-
-hipError_t nv_commit_launch(const NvParams &p, int slot, hipStream_t s) {
-    if (p.cm.N == 0 || !p.ahead) return hipSuccess;
-    hipLaunchKernelGGL(nv_commit_kernel, dim3(grid_for(p.cm.N, 256)), dim3(256), 0, s, p, slot ^ 1);
-    return hipGetLastError();
-}
-
 #define NV_LT_SWITCH(L_)              \
     switch (p.L) {                    \
         case 0: L_(0); break;         \
@@ -1192,28 +1354,34 @@ hipError_t nv_commit_launch(const NvParams &p, int slot, hipStream_t s) {
         default: L_(-1); break;       \
     }
 
-hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
-                         bool &ahead, int &slot, hipStream_t s) {
-    if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
+// The step / rollout dispatch of one demand stream: RG = Pcg (numpy's PCG64,
+// parity) or PhiloxGen (the fast stream; instantiated in newsvendor_ph.hip).
+// The fast stream's lookahead cache holds demands only: it is never committed,
+// and any other launch leaves it stale (the launch-step counter moves past it).
+template <class RG>
+hipError_t nv_launch_rg(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
+                        bool &ahead, int &slot, hipStream_t s) {
+    constexpr bool ph = RG::kCounter;
     const size_t lds = (size_t)((EPW * (p.L + 5) + 3) / 4) * 4 * sizeof(float) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
-    const bool ph = p.cm.philox != 0;       // fast stream: the run kernels only (no lookahead, no stream waves)
-    const bool la = p.ahead && nv_ahead_enabled() && !ph;
+    const bool la = p.ahead && nv_ahead_enabled();
     if (la && !pol && io.K == 1 && t_u >= 0 && t_u < p.step_limit && io.obs &&
         !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.step_limit)) {
         const bool produce = t_u + 1 < p.step_limit;
         if (ahead || produce) {
             const bool hit = ahead;
-            const int gla = hit ? (produce ? 2 : 1) * (int)grid_for(p.cm.N, WAVE) : 0;
+            // lookahead workgroups: two per 64 envs (one per sampler branch) to
+            // draw, one to commit the parity stream's state when the chain ends
+            const int gla = hit ? (produce ? 2 : (ph ? 0 : 1)) * (int)grid_for(p.cm.N, WAVE) : 0;
             const dim3 grid2(grid.x + gla);
             const int cur = slot;
 #define S_(X)                                                                                                \
     do {                                                                                                     \
-        if (hit && produce) hipLaunchKernelGGL((nv_step1_kernel<X, true, true>), grid2, block, lds, s, p, t_u, io, cur, gla);  \
-        else if (hit) hipLaunchKernelGGL((nv_step1_kernel<X, true, false>), grid2, block, lds, s, p, t_u, io, cur, gla);       \
-        else hipLaunchKernelGGL((nv_step1_kernel<X, false, true>), grid2, block, lds, s, p, t_u, io, cur, gla);                \
+        if (hit && produce) hipLaunchKernelGGL((nv_step1_kernel<X, true, true, RG>), grid2, block, lds, s, p, t_u, io, cur, gla);  \
+        else if (hit) hipLaunchKernelGGL((nv_step1_kernel<X, true, false, RG>), grid2, block, lds, s, p, t_u, io, cur, gla);       \
+        else hipLaunchKernelGGL((nv_step1_kernel<X, false, true, RG>), grid2, block, lds, s, p, t_u, io, cur, gla);                \
     } while (0)
             NV_LT_SWITCH(S_)
 #undef S_
@@ -1227,30 +1395,26 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
         }
     }
     if (ahead) {   // the one-wave kernel reads cm.rng: commit, the cache ends
-        const hipError_t ce = nv_commit_launch(p, slot, s);
+        const hipError_t ce = ph ? hipSuccess : nv_commit_launch(p, slot, s);
         ahead = false;
         if (ce != hipSuccess) return ce;
     }
-    if (!ph && (!pol || nv_pol_roll_enabled()) && io.K > 1 && t_u >= 0 && p.L > 0 &&
+    if ((!pol || nv_pol_roll_enabled()) && io.K > 1 && t_u >= 0 && p.L > 0 &&
         p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
         const dim3 gr(grid_for(p.cm.N, WAVE)), br(3 * WAVE);
         bool done = true;
 #define R_(X)                                                                                              \
     do {                                                                                                   \
         if (X > 0) {                                                                                       \
-            if (pol) hipLaunchKernelGGL((nv_roll_kernel<(X > 0 ? X : 1), true>), gr, br, NvRoll<(X > 0 ? X : 1)>::lds(), s, p, t_u, io, pv); \
-            else hipLaunchKernelGGL((nv_roll_kernel<(X > 0 ? X : 1), false>), gr, br, NvRoll<(X > 0 ? X : 1)>::lds(), s, p, t_u, io, pv); \
+            if (pol) hipLaunchKernelGGL((nv_roll_kernel<(X > 0 ? X : 1), true, RG>), gr, br, NvRoll<(X > 0 ? X : 1)>::lds(), s, p, t_u, io, pv); \
+            else hipLaunchKernelGGL((nv_roll_kernel<(X > 0 ? X : 1), false, RG>), gr, br, NvRoll<(X > 0 ? X : 1)>::lds(), s, p, t_u, io, pv); \
         } else done = false;                                                                               \
     } while (0)
         NV_LT_SWITCH(R_)
 #undef R_
         if (done) return hipGetLastError();
     }
-#define K_(X, TU, ONE, POL)                                                                              \
-    do {                                                                                                 \
-        if (ph) hipLaunchKernelGGL((nv_run_kernel<X, TU, ONE, POL, PhiloxGen>), grid, block, lds, s, p, t_u, io, pv); \
-        else hipLaunchKernelGGL((nv_run_kernel<X, TU, ONE, POL, Pcg>), grid, block, lds, s, p, t_u, io, pv);         \
-    } while (0)
+#define K_(X, TU, ONE, POL) hipLaunchKernelGGL((nv_run_kernel<X, TU, ONE, POL, RG>), grid, block, lds, s, p, t_u, io, pv)
 #define L_(X)                                          \
     do {                                               \
         if (pol) {                                     \
@@ -1270,6 +1434,32 @@ hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const 
     return hipGetLastError();
 }
 
+}  // namespace
+
+#ifdef INVSIM_NV_FAST_TU
+// newsvendor_ph.hip: this file compiled a second time for the fast-stream
+// kernels (a TU of their own, so the two instantiation sets compile in parallel)
+hipError_t nv_run_launch_ph(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
+                            bool &ahead, int &slot, hipStream_t s) {
+    if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
+    return nv_launch_rg<PhiloxGen>(p, t_u, pol, io, ahead, slot, s);
+}
+
+INVSIM_PTRS_STATS_TU(nv_ph)
+#else
+hipError_t nv_commit_launch(const NvParams &p, int slot, hipStream_t s) {
+    if (p.cm.N == 0 || !p.ahead) return hipSuccess;
+    hipLaunchKernelGGL(nv_commit_kernel, dim3(grid_for(p.cm.N, 256)), dim3(256), 0, s, p, slot ^ 1);
+    return hipGetLastError();
+}
+
+hipError_t nv_run_launch(const NvParams &p, int t_u, const PolicyIO *pol, const StepIO<float, float> &io,
+                         bool &ahead, int &slot, hipStream_t s) {
+    if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
+    if (p.cm.philox) return nv_run_launch_ph(p, t_u, pol, io, ahead, slot, s);   // newsvendor_ph.hip
+    return nv_launch_rg<Pcg>(p, t_u, pol, io, ahead, slot, s);
+}
+
 hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, hipStream_t s) {
     if (p.cm.N == 0) return hipSuccess;
     hipLaunchKernelGGL(nv_reset_kernel, dim3(grid_for(p.cm.N, 256)), dim3(256), 0, s, p, mask, obs);
@@ -1277,10 +1467,11 @@ hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, h
 }
 
 INVSIM_PTRS_STATS_TU(nv)
+#endif
 
 }  // namespace invsim
 
-#ifdef INVSIM_TIMING
+#if defined(INVSIM_TIMING) && !defined(INVSIM_NV_FAST_TU)
 extern "C" int invsim_debug_timing_nv(void *dst, int64_t bytes) {
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_tbuf), (size_t)bytes, 0, hipMemcpyDeviceToHost);
 }

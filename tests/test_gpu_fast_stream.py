@@ -278,3 +278,89 @@ def test_fast_stream_net_fused_kernels_equal_spec_kernel(gpu, monkeypatch, graph
     for i, (x, y) in enumerate(zip(a, b)):
         assert torch.equal(x.view(torch.uint8) if x.dtype == torch.float64 else x,
                            y.view(torch.uint8) if y.dtype == torch.float64 else y), i
+
+
+def _nv_fast_run(gpu, n, fused, monkeypatch, L=5, limit=40, mu_max=200.0):
+    import invsim
+    for v in ("INVSIM_NV_AHEAD", "INVSIM_NV_ROLL", "INVSIM_NV_POL_ROLL"):
+        monkeypatch.setenv(v, "1" if fused else "0")
+    env = invsim.NewsvendorEnv(n, device=gpu, lead_time=L, step_limit=limit, mu_max=mu_max,
+                               demand_stream="philox", record_demand=True)
+    env.reset(seed=29)
+    gen = torch.Generator(device=gpu)
+    gen.manual_seed(8)
+    out = []
+    for k in range(limit + 6):                             # lookahead steps, across the NEXT_STEP reset
+        a = torch.rand((n, 1), device=gpu, generator=gen) * 150
+        o, r, te, tr, info = env.step(a)
+        out += [o.clone(), r.clone(), tr.clone(), info["demand"].clone()]
+    acts = torch.rand((2 * limit + 7, n, 1), device=gpu, generator=gen) * 150
+    out += list(env.rollout(acts))                         # 3-wave rollout kernel, resets mid-launch
+    for ag in (invsim.OrderUpToHeuristicAgent(1.2), invsim.ClassicNewsvendorAgent("profit_margin", 0.9)):
+        m = torch.zeros((n, 2), dtype=torch.float64, device=gpu)
+        pol = env.rollout_policy(ag, limit + 9, obs=True, actions=True, metrics=m)
+        out += [pol[k] for k in sorted(pol)] + [m]
+    for k in range(3):                                     # steps after a rollout: a new lookahead chain
+        a = torch.rand((n, 1), device=gpu, generator=gen) * 150
+        o, r, te, tr, info = env.step(a)
+        out += [o.clone(), r.clone(), info["demand"].clone()]
+    out.append(env.get_state())
+    return out
+
+
+@pytest.mark.parametrize("n,L,limit,mu_max", [(4096, 5, 40, 200.0), (65536, 5, 40, 200.0),
+                                              (5000, 2, 12, 14.0), (3000, 9, 17, 200.0)])
+def test_fast_stream_newsvendor_fused_kernels_equal_run_kernel(gpu, monkeypatch, n, L, limit, mu_max):
+    """Newsvendor on the fast stream: the lookahead step kernel (demand-only
+    cache), the 3-wave rollout kernel (PTRS wave positioned per launch step,
+    multiplication draws spread over the wave's lanes) and its in-kernel agents
+    give nv_run_kernel's results bit for bit.  mu_max = 14 puts ~70 % of the
+    episodes on the multiplication branch (more than the parity kernel's
+    16-env lane groups)."""
+    a = _nv_fast_run(gpu, n, True, monkeypatch, L, limit, mu_max)
+    b = _nv_fast_run(gpu, n, False, monkeypatch, L, limit, mu_max)
+    assert len(a) == len(b)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x.view(torch.uint8) if x.dtype == torch.float64 else x,
+                           y.view(torch.uint8) if y.dtype == torch.float64 else y), i
+
+
+def _nv_switch_seq(gpu, monkeypatch, ahead):
+    import invsim
+    monkeypatch.setenv("INVSIM_NV_AHEAD", "1" if ahead else "0")
+    n = 2048
+    env = invsim.NewsvendorEnv(n, device=gpu, record_demand=True)
+    env.reset(seed=23)
+    a = torch.full((n, 1), 40.0, device=gpu)
+    out = []
+
+    def steps(k):
+        for _ in range(k):
+            o, r, _, _, info = env.step(a)
+            out.extend([o.clone(), r.clone(), info["demand"].clone()])
+    steps(3)                                    # numpy, its lookahead cache live
+    env.set_demand_stream("philox")
+    steps(4)                                    # fast stream, its demand-only cache live
+    out.append(env.get_state().clone())         # the PCG64 states untouched
+    steps(2)
+    blob = env.get_state().clone()
+    steps(3)
+    env.set_state(blob)                         # counter from the blob; the cache dropped
+    steps(3)
+    env.reset()                                 # the reset's own counter value
+    steps(2)
+    env.set_demand_stream("numpy")
+    steps(4)
+    env.reset(seed=5)
+    env.set_demand_stream("philox")
+    steps(2)
+    out.append(env.get_state().clone())
+    return out
+
+
+def test_fast_stream_newsvendor_lookahead_across_switches_and_checkpoints(gpu, monkeypatch):
+    a = _nv_switch_seq(gpu, monkeypatch, True)
+    b = _nv_switch_seq(gpu, monkeypatch, False)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x.view(torch.uint8) if x.dtype == torch.float64 else x,
+                           y.view(torch.uint8) if y.dtype == torch.float64 else y), i
