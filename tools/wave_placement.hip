@@ -67,5 +67,36 @@ int main(int argc, char **argv) {
     printf("waves/wg=%d wgs=%d: wgs with all waves on one SIMD=%d, on distinct SIMDs=%d; "
            "SIMDs used=%zu, max waves on a SIMD=%d\n",
            wpg, nwg, same_simd, wgs_multi_simd, simd_load.size(), maxl);
+    // the SIMD pattern of a workgroup's waves, relative to its wave 0 ((simd_k - simd_0) mod 4)
+    std::map<std::vector<int>, int> pat;
+    for (int g = 0; g < nwg; g++) {
+        std::vector<int> v;
+        const int s0 = (h[2 * (g * wpg)] >> 4) & 3;
+        for (int k = 0; k < wpg; k++) v.push_back((((h[2 * (g * wpg + k)] >> 4) & 3) - s0 + 4) & 3);
+        pat[v]++;
+    }
+    printf("  wave -> SIMD patterns (relative to wave 0):");
+    for (auto &kv : pat) {
+        printf(" [");
+        for (int x : kv.first) printf("%d", x);
+        printf("]x%d", kv.second);
+    }
+    printf("\n");
+    // per CU: how many waves of role k (wave index k mod roles) share a SIMD with another of the same role
+    const int roles = argc > 3 ? atoi(argv[3]) : wpg;
+    std::map<long, int> role_simd;   // (cu-simd, role) -> count
+    for (int g = 0; g < nwg; g++)
+        for (int k = 0; k < wpg; k++) {
+            const unsigned hw = h[2 * (g * wpg + k)], xcc = h[2 * (g * wpg + k) + 1] & 0xf;
+            const int simd = (hw >> 4) & 3, cu = (hw >> 8) & 15, sh = (hw >> 12) & 1, se = (hw >> 13) & 7;
+            role_simd[((((long)xcc * 8 + se) * 2 + sh) * 64 + cu * 4 + simd) * 16 + (k % roles)]++;
+        }
+    std::map<int, std::map<int, int>> rh;   // role -> (waves of that role on one SIMD -> SIMDs)
+    for (auto &kv : role_simd) rh[(int)(kv.first % 16)][kv.second]++;
+    for (auto &r : rh) {
+        printf("  role %d: SIMDs holding n waves of it:", r.first);
+        for (auto &kv : r.second) printf(" %dx%d", kv.first, kv.second);
+        printf("\n");
+    }
     return 0;
 }
