@@ -1302,21 +1302,30 @@ struct ImLt3o : ImLt3<L0, L1, L2> {
 // computes each step's order from I and its own register history of the last
 // L_i orders per stage (hv), and hands the orders to the obs wave in LDS (abuf)
 // beside the inventory; outputs optional, metrics in registers (as im_roll3_kernel).
-template <int L0, int L1, int L2, bool BACKLOG, bool POL, class RG = Pcg>
-__global__ void __launch_bounds__(3 * WAVE)
+// G2 = 2 (INVSIM_IM_ROLL3O_G2=1, A/B): two 64-env groups per 6-wave
+// workgroup.  The dispatcher puts waves w and w + 4 of a 6-wave workgroup on
+// one SIMD and waves 2 and 3 on a SIMD each (tools/wave_placement,
+// profiles/r03/launch/placement.txt), so the two dynamics waves take waves 2
+// and 3 and every demand wave shares its SIMD with the other group's obs wave.
+template <int L0, int L1, int L2, bool BACKLOG, bool POL, class RG = Pcg, int G2 = 1>
+__global__ void __launch_bounds__(3 * WAVE * G2)
 im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     using G = ImLt3o<L0, L1, L2>;
     constexpr int M1 = G::M1, D = G::D, O = G::O, CH = G::CH;
-    extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
+    extern __shared__ __attribute__((aligned(16))) int64_t im_lds3o[];
+    const int w = threadIdx.x / WAVE;
+    // G2 = 2: wave -> (role, group) = 0 (0,0) 1 (0,1) 2 (1,0) 3 (1,1) 4 (2,1) 5 (2,0)
+    const int role = G2 == 1 ? w : (w >> 1);
+    const int grp = G2 == 1 ? 0 : (w < 4 ? (w & 1) : ((w & 1) ^ 1));
+    int64_t *im_tile = im_lds3o + (int64_t)grp * (int64_t)(G::lds(POL) / sizeof(int64_t));
     double *rhs_l = reinterpret_cast<double *>(im_tile + WAVE * O);
     int64_t *dbuf = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);   // [RD * CH][WAVE]
     int64_t *ibuf = dbuf + G::RD * CH * WAVE;                             // [2][CH][M1][WAVE]
     int64_t *abuf = ibuf + 2 * CH * M1 * WAVE;                            // POL: [2][CH][M1][WAVE]
     const int lane = threadIdx.x & (WAVE - 1);
-    const int role = threadIdx.x / WAVE;
     const int64_t N = P.cm.N;
     const int64_t S = P.cm.Npad;
-    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e0 = ((int64_t)blockIdx.x * G2 + grp) * WAVE;
     const int64_t e = e0 + lane;
     const bool valid = e < N;
     const int64_t el = valid ? e : N - 1;          // padded lanes: the last env's data, never stored
@@ -1662,6 +1671,13 @@ inline int64_t im_roll3o_max_n() {
     return v ? (int64_t)atoll(v) : 32768;
 }
 
+// INVSIM_IM_ROLL3O_G2=1: two 64-env groups per 6-wave workgroup (A/B; measured
+// equal on LostSales 32768, profiles/r03/launch/g2_stage.txt)
+inline bool im_roll3o_g2() {
+    const char *v = getenv("INVSIM_IM_ROLL3O_G2");
+    return v && v[0] == '1';
+}
+
 inline bool im_roll_enabled() {
     const char *s = getenv("INVSIM_IM_ROLL");
     return !(s && s[0] == '0');
@@ -1708,9 +1724,13 @@ hipError_t im_roll_launch(const ImParams &p, bool backlog, int t_u, const Policy
     // LostSales 32768 envs 87.5 -> 77.7 us per K = 30; at 65536 the
     // 2-role kernel is faster, 118 vs 152 us)
     const bool three = p.cm.N <= im_roll3o_max_n();
+    // two groups per workgroup when the group count is even (every workgroup full)
+    const bool two = three && im_roll3o_g2() && (g3.x % 2) == 0;
+    const dim3 g6(g3.x / 2);
 #define R_(B, POL)                                                                                                    \
     do {                                                                                                              \
-        if (three) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, B, POL, RG>), g3, dim3(3 * WAVE), G3::lds(POL), s, p, t_u, io, pv); \
+        if (two) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, B, POL, RG, 2>), g6, dim3(6 * WAVE), 2 * G3::lds(POL), s, p, t_u, io, pv); \
+        else if (three) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, B, POL, RG>), g3, dim3(3 * WAVE), G3::lds(POL), s, p, t_u, io, pv); \
         else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, B, POL, RG>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);            \
     } while (0)
     if (pol) {

@@ -937,15 +937,19 @@ def test_net_demand_lookahead_mixed_calls(gpu, graph, kw, monkeypatch):
 @pytest.mark.parametrize("cls,n,periods", [("InvManagementBacklogEnv", 3000, 30),
                                            ("InvManagementLostSalesEnv", 32768, 30),
                                            ("InvManagementBacklogEnv", 3000, 20),
-                                           ("InvManagementBacklogEnv", 3000, 12)])
+                                           ("InvManagementBacklogEnv", 3000, 12),
+                                           ("InvManagementBacklogEnv", 4090, 30)])
 def test_invmgmt_three_role_rollout_equals_two_role(gpu, monkeypatch, cls, n, periods):
     """Small batches run im_roll3o_kernel (obs work on a third wave); forcing
     INVSIM_IM_ROLL3O_MAX_N=0 keeps them on im_roll3_kernel.  Same state in:
-    identical outputs, demand record and state out.  A last case with the
-    one-wave kernel (INVSIM_IM_ROLL=0) pins both against a slot per step."""
+    identical outputs, demand record and state out.  A case with the one-wave
+    kernel (INVSIM_IM_ROLL=0) pins both against a slot per step, and one with
+    INVSIM_IM_ROLL3O_G2=1 runs two groups per 6-wave workgroup (an even group
+    count: 32 768 envs, and 4 090 whose last group is partial; odd counts fall
+    back to one group)."""
     import invsim
     envs = []
-    for i in range(3):
+    for i in range(4):
         env = getattr(invsim, cls)(n, device=gpu, record_demand=True, periods=periods)
         env.reset(seed=17)
         envs.append(env)
@@ -959,11 +963,14 @@ def test_invmgmt_three_role_rollout_equals_two_role(gpu, monkeypatch, cls, n, pe
                 monkeypatch.setenv("INVSIM_IM_ROLL3O_MAX_N", "0")
             if i == 2:
                 monkeypatch.setenv("INVSIM_IM_ROLL", "0")
+            if i == 3:
+                monkeypatch.setenv("INVSIM_IM_ROLL3O_G2", "1")
             outs.append(env.rollout(a))
             dems.append(env._demand.clone())
             monkeypatch.delenv("INVSIM_IM_ROLL3O_MAX_N", raising=False)
             monkeypatch.delenv("INVSIM_IM_ROLL", raising=False)
-        for j in (1, 2):
+            monkeypatch.delenv("INVSIM_IM_ROLL3O_G2", raising=False)
+        for j in (1, 2, 3):
             for x, y in zip(outs[0], outs[j]):
                 assert torch.equal(x, y), (K, j)
             assert torch.equal(dems[0], dems[j])
