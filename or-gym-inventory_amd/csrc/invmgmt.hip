@@ -766,6 +766,7 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
             }
         }
         wg_lds_sync();   // d and the window rows -> dynamics wave
+        TPROBE(6);       // the window wave past its first barrier
         if constexpr (!RG::kCounter) {
             if (!AHEAD && valid) {   // committed generator state: after this step's draw
                 if (Acur) {          // into slot cur (the committed slot once the slots flip)
@@ -839,6 +840,7 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         U[i + 1] = wrap_sub(ordreq[i], R[i]);                       // :304
     }
     wg_lds_sync();   // d from the demand wave
+    TPROBE_AT(1, WAVE);   // the dynamics wave: loads in, d handed over
     const int64_t d = dsh[lane];
     const int64_t dfill = wrap_add(d, B[0]);                        // :284-286
     const int64_t s0 = Icur[0] < dfill ? Icur[0] : dfill;           // :288
@@ -862,6 +864,7 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         for (int i = 0; i < M1; i++) w[(n - 1) * M1 + i] = req[i];  // newest row last (:380)
     }
     wg_lds_sync();   // tile complete
+    TPROBE_AT(2, WAVE);   // the dynamics wave: step computed, stores next
     {
         const int64_t h = thalf < tcount ? thalf : tcount;
         if (tcount > h)

@@ -424,13 +424,15 @@ def test_policy_on_fused_rollout_equals_run_kernel(gpu, monkeypatch, cls, agent,
     """BaseStock / ConstantOrder inside the fused 2-role rollout kernel
     (im_roll3_kernel<..., POL>) give the one-wave run kernel's outputs, actions,
     metrics and final state bit for bit, across NEXT_STEP autoresets and
-    chained launches (every output optional)."""
+    chained launches (every output optional).  At 4 096 envs the 3-role
+    kernel runs, once more with two groups per workgroup (INVSIM_IM_ROLL3O_G2)."""
     import torch
     import invsim
     ag = invsim.ConstantOrderAgent(0.3) if agent == "constant" else invsim.BaseStockAgent(float(agent[-3:]))
     res = []
-    for roll in ("1", "0"):
-        monkeypatch.setenv("INVSIM_IM_POL_ROLL", roll)
+    for roll in ("0", "1", "g2"):
+        monkeypatch.setenv("INVSIM_IM_POL_ROLL", "0" if roll == "0" else "1")
+        monkeypatch.setenv("INVSIM_IM_ROLL3O_G2", "1" if roll == "g2" else "0")
         env = getattr(invsim, cls)(n, device=gpu)
         env.reset(seed=21)
         m = torch.zeros((n, 6), dtype=torch.float64, device=gpu)
@@ -438,13 +440,14 @@ def test_policy_on_fused_rollout_equals_run_kernel(gpu, monkeypatch, cls, agent,
         b = env.rollout_policy(ag, 40, obs=False, rewards=False, metrics=m)
         c = env.rollout_policy(ag, 30, obs=True, metrics=m)
         res.append((a, b, c, m, env.get_state()))
-    (a1, b1, c1, m1, s1), (a2, b2, c2, m2, s2) = res
-    for k in a1:
-        assert torch.equal(a1[k], a2[k]), k
-    for k in c1:
-        assert torch.equal(c1[k], c2[k]), k
-    assert torch.equal(m1.view(torch.int64), m2.view(torch.int64))
-    assert torch.equal(s1, s2)
+    a2, b2, c2, m2, s2 = res[0]                       # the one-wave run kernel
+    for a1, b1, c1, m1, s1 in res[1:]:
+        for k in a1:
+            assert torch.equal(a1[k], a2[k]), k
+        for k in c1:
+            assert torch.equal(c1[k], c2[k]), k
+        assert torch.equal(m1.view(torch.int64), m2.view(torch.int64))
+        assert torch.equal(s1, s2)
 
 
 @pytest.mark.gpu
