@@ -735,9 +735,14 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
             const int rmax = nw > 0 ? nw / M1 - 1 : 0;
 #pragma unroll
             for (int r = 0; r < WL / M1; r++) {
+#ifdef INVSIM_ABL_NO_WINDOW   // profiling ablation build only (wrong results): no window read
+#pragma unroll
+                for (int i = 0; i < M1; i++) wv[r * M1 + i] = (uint32_t)(r + i);
+#else
                 const uint32_t *src = P.alog32 + wrow(r < rmax ? r : rmax);
 #pragma unroll
                 for (int i = 0; i < M1; i++) wv[r * M1 + i] = src[i];
+#endif
             }
         }
         if (!AHEAD) {
