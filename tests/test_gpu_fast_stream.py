@@ -364,3 +364,50 @@ def test_fast_stream_newsvendor_lookahead_across_switches_and_checkpoints(gpu, m
     for i, (x, y) in enumerate(zip(a, b)):
         assert torch.equal(x.view(torch.uint8) if x.dtype == torch.float64 else x,
                            y.view(torch.uint8) if y.dtype == torch.float64 else y), i
+
+
+def test_fast_stream_newsvendor_pit_1e8(gpu):
+    """Newsvendor on the fast stream (the lookahead step kernel): each episode
+    draws mu ~ U(0, mu_max) and then Poisson(mu) demands, so the randomized
+    probability integral transform u = F(d - 1) + V (F(d) - F(d - 1)) with the
+    episode's own mu is U(0, 1) whatever mu is.  Over >= 1e8 draws: a
+    chi-square on 100 bins of u, separately for numpy's two sampler branches
+    (mu < 10: multiplication, mu >= 10: PTRS), and the mean of (d - mu) / sqrt(mu)."""
+    import invsim
+    from scipy.stats import chi2
+    n = 65536
+    env = invsim.NewsvendorEnv(n, device=gpu, record_demand=True, demand_stream="philox", copy=False)
+    env.reset(seed=13)
+    a = torch.zeros((n, 1), device=gpu)
+    gen = torch.Generator(device=gpu).manual_seed(17)
+    bins = 100
+    hist = {b: torch.zeros(bins, dtype=torch.float64, device=gpu) for b in ("mult", "ptrs")}
+    zsum = {b: torch.zeros((), dtype=torch.float64, device=gpu) for b in ("mult", "ptrs")}
+    cnt = {b: 0 for b in ("mult", "ptrs")}
+    mu = env.params()[:, 4].clone()
+    draws = 0
+    k = 0
+    while draws < 100_000_000:
+        d = env.step(a)[4]["demand"].double()
+        if k % 41 == 40:                                   # the NEXT_STEP reset call: new params, no draw
+            mu = env.params()[:, 4].clone()
+        else:
+            lo = torch.where(d > 0, torch.special.gammaincc(d, mu), torch.zeros_like(d))   # F(d - 1)
+            hi = torch.special.gammaincc(d + 1, mu)                                        # F(d)
+            u = lo + torch.rand(n, dtype=torch.float64, device=gpu, generator=gen) * (hi - lo)
+            z = (d - mu) / mu.clamp(min=1e-300).sqrt()
+            for b, m in (("mult", mu < 10), ("ptrs", mu >= 10)):
+                ub = u[m]
+                hist[b] += torch.bincount((ub * bins).long().clamp(0, bins - 1), minlength=bins).double()
+                zsum[b] += z[m].sum()
+                cnt[b] += int(m.sum())
+            draws += n
+        k += 1
+    for b in ("mult", "ptrs"):
+        h = hist[b].cpu().numpy()
+        e = cnt[b] / bins
+        stat = float(((h - e) ** 2 / e).sum())
+        p = float(chi2.sf(stat, bins - 1))
+        assert p > 1e-4, f"{b}: PIT chi-square {stat:.1f} on {bins - 1} dof, p = {p:.2e} ({cnt[b]} draws)"
+        assert abs(float(zsum[b]) / cnt[b]) < 6 / np.sqrt(cnt[b]), b
+    assert cnt["mult"] > 2_000_000 and cnt["ptrs"] > 90_000_000
