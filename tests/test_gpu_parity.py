@@ -1234,3 +1234,56 @@ def test_net_market_samplers_vs_oracle(gpu, oracle, dists):
         e_obs, e_rew, _ = orc.step(acts[k])
         assert _eq_bits(o2[k].cpu().numpy(), e_obs), f"rollout step {k}"
         _assert_reward(r2[k].cpu().numpy(), e_rew, f"rollout step {k}")
+
+
+@pytest.mark.parametrize("roll", ["3role", "2role", "oneway"])
+def test_invmgmt_wide_orders_vs_oracle(gpu, oracle, monkeypatch, roll):
+    """Requested orders at and around the 16-bit ring's sentinel (0xFFFF) and
+    past 2^32, through split steps, a rollout across the NEXT_STEP autoreset
+    (3-role, 2-role or one-wave kernel) and more split steps, against the C
+    oracle: the observation window (the action_log ring) and the rewards."""
+    import invsim
+    if roll == "2role":
+        monkeypatch.setenv("INVSIM_IM_ROLL3O_MAX_N", "0")
+    if roll == "oneway":
+        monkeypatch.setenv("INVSIM_IM_ROLL", "0")
+    n = 4096
+    env = invsim.InvManagementBacklogEnv(n, device=gpu)
+    orc = oracle.OracleInvMgmt(n, backlog=True)
+    orc.seed(range(50, 50 + n))
+    orc.reset()
+    env.reset(seed=50)
+    rng = np.random.default_rng(9)
+    special = np.array([65534, 65535, 65536, 2 ** 32 - 2, 2 ** 32 - 1, 2 ** 32, 2 ** 40], dtype=np.int64)
+
+    def acts():
+        a = rng.integers(-5, 300, size=(n, 3)).astype(np.int64)
+        m = rng.random((n, 3)) < 0.15
+        a[m] = special[rng.integers(0, len(special), size=int(m.sum()))]
+        return a
+    t = 0
+
+    def check(o, r, a, what):
+        nonlocal t
+        if t == 30:                                        # the NEXT_STEP autoreset step
+            e_obs = orc.reset()
+            assert np.array_equal(o, e_obs), what
+            t = 0
+            return
+        e_obs, e_rew, _ = orc.step(a)
+        assert np.array_equal(o, e_obs), what
+        _assert_reward(r, e_rew, what)
+        t += 1
+    for s in range(12):
+        a = acts()
+        o, r, _, _, _ = env.step(torch.from_numpy(a).to(gpu))
+        check(o.cpu().numpy(), r.cpu().numpy(), a, f"step {s}")
+    A = np.stack([acts() for _ in range(25)])
+    ro, rr, _, _ = env.rollout(torch.from_numpy(A).to(gpu))
+    ro, rr = ro.cpu().numpy(), rr.cpu().numpy()
+    for k in range(25):
+        check(ro[k], rr[k], A[k], f"rollout step {k}")
+    for s in range(10):
+        a = acts()
+        o, r, _, _, _ = env.step(torch.from_numpy(a).to(gpu))
+        check(o.cpu().numpy(), r.cpu().numpy(), a, f"step {12 + 25 + s}")
