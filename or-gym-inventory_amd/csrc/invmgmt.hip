@@ -1679,11 +1679,15 @@ inline int64_t im_roll3o_max_n() {
     return v ? (int64_t)atoll(v) : 32768;
 }
 
-// INVSIM_IM_ROLL3O_G2=1: two 64-env groups per 6-wave workgroup (A/B; measured
-// equal on LostSales 32768, profiles/r03/launch/g2_stage.txt)
-inline bool im_roll3o_g2() {
+// Two 64-env groups per 6-wave workgroup: the default for policy rollouts
+// (BaseStock at 32 768 envs: 63.1-64.8 against 66.5-67.7 us per 30 steps),
+// equal open loop (profiles/r03/launch/g2_stage.txt).  INVSIM_IM_ROLL3O_G2=1 /
+// =0 forces it on / off for both (A/B, tests).
+inline bool im_roll3o_g2(bool pol) {
     const char *v = getenv("INVSIM_IM_ROLL3O_G2");
-    return v && v[0] == '1';
+    if (v && v[0] == '1') return true;
+    if (v && v[0] == '0') return false;
+    return pol;
 }
 
 inline bool im_roll_enabled() {
@@ -1733,7 +1737,7 @@ hipError_t im_roll_launch(const ImParams &p, bool backlog, int t_u, const Policy
     // 2-role kernel is faster, 118 vs 152 us)
     const bool three = p.cm.N <= im_roll3o_max_n();
     // two groups per workgroup when the group count is even (every workgroup full)
-    const bool two = three && im_roll3o_g2() && (g3.x % 2) == 0;
+    const bool two = three && im_roll3o_g2(pol != nullptr) && (g3.x % 2) == 0;
     const dim3 g6(g3.x / 2);
 #define R_(B, POL)                                                                                                    \
     do {                                                                                                              \
