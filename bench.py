@@ -9,7 +9,8 @@ The step outputs land in a [32, N] slab that the HIP episode fold
 (`invsim_episode_fold`) reduces to episodic-return statistics every 32 steps
 inside the timed region; one all-reduce of them follows the region.  After
 the step region the same handle runs a timed region of fused K=30 rollouts
-(`invsim_rollout`), reported under "rollout" in the same line.
+(`invsim_rollout`), reported under "rollout" in the same line, and the step
+loop again as HIP-graph replays (one episode cycle per replay), under "graph".
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--mode step|rollout]
 
@@ -73,6 +74,12 @@ def parse():
                     help="episodic-return fold of the timed outputs: between blocks on the kernel stream "
                          "(default), on a side stream (measured slower: it shares the CUs with the step "
                          "kernels), or off (A/B only: no episode_stats)")
+    ap.add_argument("--stop", default="event", choices=["event", "sync"],
+                    help="end of the timed region: the kernel stream's last event completing (default), or "
+                         "torch.cuda.synchronize returning; the region is closed by torch.cuda.synchronize "
+                         "either way")
+    ap.add_argument("--no-graph-line", action="store_true",
+                    help="step mode: skip the HIP-graph replay region reported under 'graph'")
     ap.add_argument("--no-rollout-line", action="store_true",
                     help="step mode: skip the K-step rollout region reported under 'rollout'")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
@@ -186,11 +193,16 @@ def _fold_rows(stats, rew, term, trunc, rows, sp):
 
 def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     """Warm up, then time `steps` env.step()s of the whole batch (mode "step":
-    one invsim_step each; "rollout": invsim_rollout launches of K steps), with
-    barrier + synchronize on both sides and the max over ranks.  The step
-    outputs are written into [R, N] slabs that the HIP episode fold
-    (invsim_episode_fold) reduces every R steps inside the timed region, on a
-    side stream; the statistics are all-reduced once after it."""
+    one invsim_step each; "rollout": invsim_rollout launches of K steps;
+    "policy": invsim_rollout_policy launches), with barrier + synchronize on
+    both sides and the max over ranks.  The step outputs are written into
+    [R, N] slabs that the HIP episode fold (invsim_episode_fold) reduces every
+    R steps inside the timed region, on the kernel stream between blocks
+    (--fold inline, the default; --fold side is the measured-slower side-stream
+    variant); the statistics are all-reduced once after the region.  The clock
+    stops when the kernel stream's last event completes (--stop event) or at
+    the return of torch.cuda.synchronize (--stop sync); torch.cuda.synchronize
+    closes the region either way."""
     import torch
     import invsim
     from invsim.distributed import EpisodeStats
@@ -275,6 +287,8 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     for a, b in evs:
         a.record(stream)
         b.record(stream)
+    end_ev = torch.cuda.Event()
+    end_ev.record(stream)
     blk = [0]
 
     def region(n_calls, timed):
@@ -301,18 +315,28 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     region(warm, False)
     torch.cuda.synchronize(dev)
     stats.reset_acc()                  # count the episodes that finish in the timed region
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     region(calls, True)
-    torch.cuda.synchronize(dev)
-    if world > 1:
+    if args.stop == "event":
+        # every timed launch and fold is on `stream`: its last event completing
+        # is the end of the work (hipEventSynchronize, no device-wide drain)
+        end_ev.record(stream)
+        end_ev.synchronize()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize(dev)
+    else:
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+    if dist.is_initialized():
         dist.barrier()
-    el = time.perf_counter() - t0
-    backend = dist.get_backend() if world > 1 else None
+        t1 = time.perf_counter()
+    el = t1 - t0
+    backend = dist.get_backend() if dist.is_initialized() else None
     cdev = dev if backend == "nccl" else torch.device("cpu")
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -328,6 +352,76 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     achieved_wall = B * N * total_steps / el / 1e9
     return dict(el=el, calls=calls, warm=warm, steps_per_call=steps_per_call, total_steps=total_steps,
                 N=N, K=K, B=B, kern_ms=kern_ms, achieved=achieved, achieved_wall=achieved_wall, ep=ep)
+
+
+def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
+    """The step region as HIP-graph replays ("hipEvent around K
+    launches (or a graph replay)"), reported beside the eager step line: one
+    replay = one episode cycle, periods + 1 invsim_step calls under NEXT_STEP
+    (each writing its row of a [C, N] output slab) and the episode fold of the
+    slab, recorded once with invsim.graphs.StepGraph.  ceil(steps / C) replays,
+    barrier + synchronize around them, max over ranks; one hipGraphLaunch per
+    cycle takes host submission out of the loop."""
+    import torch
+    import invsim
+    from invsim.distributed import EpisodeStats
+    from invsim.graphs import StepGraph
+    lib, h = env._lib, env._h
+    N, O = env.num_envs, env.obs_dim
+    C = env._horizon() + 1
+    pool = max(1, args.pool)
+    acts = make_actions(env, pool, 0, gen)
+    rew = torch.empty((C, N), dtype=torch.float64, device=dev)
+    term = torch.empty((C, N), dtype=torch.bool, device=dev)
+    trunc = torch.empty((C, N), dtype=torch.bool, device=dev)
+    obs = torch.empty((N, O), dtype=env.obs_dtype, device=dev)
+    stats = EpisodeStats(N, dev)
+
+    def cycle():
+        sp = torch._C._cuda_getCurrentRawStream(dev.index)
+        for i in range(C):
+            rc = lib.invsim_step(h, acts[i % pool].data_ptr(), obs.data_ptr(), rew[i].data_ptr(),
+                                 term[i].data_ptr(), trunc[i].data_ptr(), None, sp)
+            if rc:
+                raise RuntimeError(invsim._capi.last_error(h))
+        stats.update_block(rew, term, trunc, stream=sp)
+    g = StepGraph(env, cycle, warmup=1)
+    reps = max(1, -(-steps // C))
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    e1.record(stream)
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    stats.reset_acc()
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(reps):
+        g.replay()
+    e1.record(stream)
+    e1.synchronize()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize(dev)
+    if dist.is_initialized():
+        dist.barrier()
+        t1 = time.perf_counter()
+    el = t1 - t0
+    if dist.is_initialized():
+        cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([el], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ep = stats.allreduce()
+    total = reps * C
+    return {"value": total * N * world / el, "unit": "env-steps/s", "steps": total, "replays": reps,
+            "steps_per_replay": C, "ms_per_step": el * 1e3 / total,
+            "event_ms_per_step": e0.elapsed_time(e1) / total,
+            "what": "invsim_step x (periods+1) + episode fold per replay, one HIP graph (StepGraph)",
+            "episode_stats": dict(ep, source="the replays' own episode fold, one all-reduce after the region")}
 
 
 def _roofline(r, traffic, traffic_src):
@@ -373,7 +467,10 @@ def main():
     # RCCL ("nccl") over xGMI, one rank per GPU; INVSIM_BENCH_BACKEND=gloo
     # rehearses the multi-rank path with several ranks on one GPU
     backend = os.environ.get("INVSIM_BENCH_BACKEND", "nccl")
-    if world > 1:
+    # a process group whenever torch.distributed.run started this process (also
+    # a 1-rank one: it runs the same RCCL calls an 8-GPU node makes); none for a
+    # plain `python bench.py`
+    if "WORLD_SIZE" in os.environ:
         ndev = torch.cuda.device_count()
         if backend == "nccl":
             if local >= ndev:
@@ -407,7 +504,7 @@ def main():
         "value": r["total_steps"] * N * world / r["el"],
         "unit": "env-steps/s",
         "n_gpus": world,
-        "ranks": dist.get_world_size() if world > 1 else 1,
+        "ranks": dist.get_world_size() if dist.is_initialized() else 1,
         "steps": r["total_steps"],
         "warmup": r["warm"] * r["steps_per_call"],
         "ms_per_step": r["el"] * 1e3 / r["total_steps"],
@@ -421,25 +518,40 @@ def main():
                            (f" agent={wl['agent'][0]}({wl['agent'][1]})" if args.mode == "policy" else ""),
                    "autoreset": "next_step",
                    "parallelism": f"dp{world} (env sharding, no data-path collective)",
-                   "backend": (backend if world > 1 else None), "demand_stream": args.demand_stream},
+                   "backend": (backend if dist.is_initialized() else None), "demand_stream": args.demand_stream},
         "roofline": _roofline(r, traffic, traffic_src),
         "episode_stats": dict(r["ep"], source="timed batch: HIP episode fold of the timed steps' rewards and "
                                               "done flags, one all-reduce after the region"),
     }
+    C = env._horizon() + 1                                  # steps per episode cycle (NEXT_STEP)
+    if r["total_steps"] < C:
+        out["episode_stats"]["note"] = (
+            f"the timed window holds {r['total_steps']} steps, fewer than one episode cycle ({C} steps: "
+            f"{C - 1} periods + the NEXT_STEP reset step), so no episode ends inside it; the rollout "
+            f"region's episode_stats cover whole cycles")
     if args.mode == "step" and not args.no_rollout_line:
-        # the fused K-step rollout of the same handle, timed the same way
-        rr = run_region(args, env, wl, "rollout", max(args.steps, 10 * args.rollout_k),
-                        2 * args.rollout_k, world, dev, gen, dist)
+        # the fused K-step rollout of the same handle, timed the same way, over a
+        # whole number of episode cycles (every env finishes the same number of
+        # episodes whatever the phase it starts in)
+        Kr = args.rollout_k
+        unit = C * Kr
+        rsteps = unit * max(1, -(-args.steps // unit))
+        rr = run_region(args, env, wl, "rollout", rsteps, 2 * Kr, world, dev, gen, dist)
         t2, s2 = _pmc(args.workload, "rollout", full)
         out["rollout"] = {"value": rr["total_steps"] * N * world / rr["el"], "unit": "env-steps/s",
                           "steps": rr["total_steps"], "launches": rr["calls"], "K": rr["K"],
                           "ms_per_launch": rr["el"] * 1e3 / rr["calls"],
-                          "roofline": _roofline(rr, t2, s2)}
+                          "roofline": _roofline(rr, t2, s2),
+                          "episode_stats": dict(rr["ep"], cycles=rr["total_steps"] // C,
+                                                source="timed rollout batch: HIP episode fold between "
+                                                       "launch blocks, one all-reduce after the region")}
+    if args.mode == "step" and not args.no_graph_line and args.demand_stream == "numpy":
+        out["graph"] = run_graph_region(args, env, wl, args.steps, world, dev, gen, dist)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     return 0
 

@@ -163,7 +163,10 @@ int invsim_set_autoreset(invsim_handle *h, int32_t mode);
 /* Seeding = gymnasium seeding.np_random(seed): numpy SeedSequence(seed) -> PCG64.
  * seed_range: env i (mask[i] != 0, or all when mask == NULL) gets the 128-bit
  * integer seed  base + first_index + i  (gymnasium SyncVectorEnv: seed + i).
- * seed_words: env i gets the little-endian uint32 entropy words[i][0..nwords[i]). */
+ * seed_words: env i gets the little-endian uint32 entropy words[i][0..nwords[i]).
+ * An unmasked seed (mask == NULL) also restarts the fast demand stream's
+ * launch-step counter (INVSIM_DEMAND_PHILOX below), so reseeding every env with
+ * the same seeds replays the same demands; a masked seed keeps the counter. */
 int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int64_t first_index,
                       const uint8_t *mask, void *stream);
 int invsim_seed_words(invsim_handle *h, const uint32_t *words /*[N][4]*/,
@@ -271,8 +274,9 @@ int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear);
  * written per step.  Every step / rollout step (and a Newsvendor reset)
  * advances the handle's launch-step counter, which get_state / set_state carry
  * ("philox_step"; the first fast-stream call after set_state reads it back,
- * synchronously).  Switching streams synchronises the device once; the PCG64
- * states are untouched by fast-stream steps. */
+ * synchronously).  Switching streams synchronises the device (work queued on
+ * any stream finishes first); the PCG64 states are untouched by fast-stream
+ * steps. */
 #define INVSIM_DEMAND_NUMPY 0
 #define INVSIM_DEMAND_PHILOX 1
 int invsim_set_demand_stream(invsim_handle *h, int32_t mode);

@@ -785,6 +785,16 @@ static int commit_rng(invsim_handle *h, hipStream_t s) {
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "rng commit");
 }
 
+// An unmasked seed restarts the fast stream's launch-step counter, so the same
+// seeds give the same demands again (gymnasium's reset(seed=s) contract); a
+// masked one keeps it, since the other envs' streams continue.
+static void ph_counter_restart(invsim_handle *h) {
+    h->ph_step = 0;
+    h->ph_from_blob = false;
+    h->cm.ph_step = 0;
+    sync_common(h);
+}
+
 int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int64_t first,
                       const uint8_t *mask, void *stream) {
     TraceRange tr_("invsim_seed_range");
@@ -795,6 +805,7 @@ int invsim_seed_range(invsim_handle *h, uint64_t base_lo, uint64_t base_hi, int6
     int rc = commit_rng(h, (hipStream_t)stream);   // a masked seed keeps the other streams
     if (rc != INVSIM_OK) return rc;
     h->la_valid = false;   // the lookahead cache follows the old streams
+    if (!mask) ph_counter_restart(h);
     hipError_t e = seed_range_launch(h->cm, base_lo, base_hi, first, mask, (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_range launch");
 }
@@ -808,6 +819,7 @@ int invsim_seed_words(invsim_handle *h, const uint32_t *words, const int32_t *nw
     int rc = commit_rng(h, (hipStream_t)stream);
     if (rc != INVSIM_OK) return rc;
     h->la_valid = false;
+    if (!mask) ph_counter_restart(h);
     hipError_t e = seed_words_launch(h->cm, words, nwords, mask, (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(h, e, "seed_words launch");
 }
@@ -1067,9 +1079,14 @@ int invsim_set_demand_stream(invsim_handle *h, int32_t mode) {
         return fail(h, INVSIM_EINVAL, "demand stream must be INVSIM_DEMAND_NUMPY or INVSIM_DEMAND_PHILOX");
     if (mode == h->demand_stream) return INVSIM_OK;
     DeviceGuard g(h->device);
+    // steps may still be queued on a caller's non-blocking stream, which the
+    // legacy stream does not wait for: drain the device before the commit reads
+    // the lookahead slot those steps write
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return hip_fail(h, e, "demand stream switch");
     int rc = commit_rng(h, nullptr);   // the parity stream's lookahead cache ends (legacy stream)
     if (rc != INVSIM_OK) return rc;
-    hipError_t e = hipStreamSynchronize(nullptr);
+    e = hipStreamSynchronize(nullptr);
     if (e != hipSuccess) return hip_fail(h, e, "demand stream switch");
     h->la_valid = false;
     h->demand_stream = mode;

@@ -35,7 +35,10 @@ class EpisodeStats:
     """
 
     def __init__(self, num_envs, device):
-        self.device = torch.device(device)
+        dev = torch.device(device)
+        if dev.type == "cuda" and dev.index is None:      # "cuda" -> the current device, explicitly
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
         self.num_envs = int(num_envs)
         self.ret = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
         self.acc = torch.zeros(4, dtype=torch.float64, device=self.device)
@@ -62,12 +65,13 @@ class EpisodeStats:
                     raise ValueError("EpisodeStats: outputs must be contiguous [K, N] tensors on the stats device")
             if reward.dtype != torch.float64 or any(f.dtype not in (torch.bool, torch.uint8) for f in flags):
                 raise TypeError("EpisodeStats: reward f64, flags bool/uint8")
-            if stream is None:
-                stream = torch._C._cuda_getCurrentRawStream(self.device.index)
             ptr = (lambda t: t.data_ptr() if t is not None else None)
-            _capi.check(_capi.lib().invsim_episode_fold(
-                reward.data_ptr(), ptr(terminated), ptr(truncated), K, N, self.ret.data_ptr(),
-                self.acc.data_ptr(), stream), None, "invsim_episode_fold")
+            with torch.cuda.device(self.device):           # the launch goes to the stats' GPU
+                if stream is None:
+                    stream = torch._C._cuda_getCurrentRawStream(self.device.index)
+                _capi.check(_capi.lib().invsim_episode_fold(
+                    reward.data_ptr(), ptr(terminated), ptr(truncated), K, N, self.ret.data_ptr(),
+                    self.acc.data_ptr(), stream), None, "invsim_episode_fold")
             return
         done = torch.zeros((K, N), dtype=torch.bool)
         for f in flags:

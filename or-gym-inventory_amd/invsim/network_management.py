@@ -19,7 +19,7 @@ import torch
 
 from . import _capi
 from .spaces import Box, batch_box
-from .topology import compile_graph, default_graph
+from .topology import classify, compile_graph, default_graph, validate_inputs
 from .vector import InvSimVectorEnv
 
 
@@ -36,6 +36,9 @@ class NetInvMgmtMasterEnv(InvSimVectorEnv):
         self.user_D = dict(user_D) if user_D is not None else {}
         self.sample_path = dict(sample_path) if sample_path is not None else {}
         self.graph = graph.copy() if graph is not None else default_graph()
+        if graph is None:                                 # :140-144 (the default graph only)
+            self.user_D.setdefault((1, 0), np.zeros(self.num_periods))
+            self.sample_path.setdefault((1, 0), False)
         cfg = dict(env_config) if env_config else {}
         cfg["backlog"] = self.backlog            # :84 — the argument wins over env_config
         for key, value in cfg.items():
@@ -43,10 +46,21 @@ class NetInvMgmtMasterEnv(InvSimVectorEnv):
                 self.graph = value.copy()
             else:
                 setattr(self, key, value)
+        # :149-163 -- market links carry their demand source on the graph
+        for link, d in self.user_D.items():
+            if link in self.graph.edges:
+                self.graph.edges[link]["user_D"] = list(d) if not isinstance(d, (list, np.ndarray)) else d
+                self.graph.edges[link]["sample_path"] = self.sample_path.get(link, False)
+        for link in classify(self.graph)[7]:
+            self.graph.edges[link].setdefault("user_D", np.zeros(self.num_periods))
+            self.graph.edges[link].setdefault("sample_path", False)
+        # :197-238 -- node / edge asserts, then the scalar ones
+        validate_inputs(self.graph, self.num_periods, self.user_D, self.sample_path)
         assert isinstance(self.backlog, bool), "backlog must be boolean"
         assert 0 < self.alpha <= 1, "alpha must be in (0, 1]"
         assert self.num_periods > 0, "num_periods must be positive"
-        self.topology = compile_graph(self.graph, self.num_periods, self.user_D, self.sample_path)
+        self.topology = compile_graph(self.graph, self.num_periods, self.user_D, self.sample_path,
+                                      validate=False)
         tp = self.topology
         self.main_nodes, self.reorder_links = tp.main_nodes, tp.reorder_links
         self.retail_links, self.network_links = tp.retail_links, tp.network_links

@@ -222,7 +222,7 @@ def evaluate_agent(agent, env_cls, env_config=None, n_episodes=100, seed_offset=
         env_dev = env.device
     finally:
         env.close()
-    if world > 1:
+    if on:      # a 1-rank group too: the same collectives an N-GPU job runs
         met = _gather_rows(met, n_episodes, world, rank, group)
         # both collectives on the env's device (RCCL), or on the host (gloo)
         dev = env_dev if dist.get_backend(group) == "nccl" else torch.device("cpu")

@@ -33,7 +33,7 @@ def default_graph(demand_lam=20):
     g.add_nodes_from([6], I0=380, C=80, o=0.012, v=1.000, h=0.011)
     g.add_nodes_from([7, 8])                                                # raw materials
     g.add_edges_from([
-        (1, 0, {"p": 2.000, "b": 0.100, "dist_param": {"lam": demand_lam}}),
+        (1, 0, {"p": 2.000, "b": 0.100, "demand_dist_func": "poisson", "dist_param": {"lam": demand_lam}}),
         (2, 1, {"L": 5, "p": 1.500, "g": 0.010}),
         (3, 1, {"L": 3, "p": 1.600, "g": 0.015}),
         (4, 2, {"L": 8, "p": 1.000, "g": 0.008}),
@@ -58,9 +58,9 @@ def custom_graph(demand_lam=20):
     g.add_nodes_from([5], I0=1200, C=80, o=0.012, v=1.000, h=0.100)
     g.add_nodes_from([6])
     g.add_edges_from([
-        (1, 0, {"p": 25.000, "b": 0.200, "dist_param": {"lam": demand_lam}}),
-        (2, 0, {"p": 25.000, "b": 0.200, "dist_param": {"lam": demand_lam}}),
-        (3, 0, {"p": 25.000, "b": 0.200, "dist_param": {"lam": demand_lam}}),
+        (1, 0, {"p": 25.000, "b": 0.200, "demand_dist_func": "poisson", "dist_param": {"lam": demand_lam}}),
+        (2, 0, {"p": 25.000, "b": 0.200, "demand_dist_func": "poisson", "dist_param": {"lam": demand_lam}}),
+        (3, 0, {"p": 25.000, "b": 0.200, "demand_dist_func": "poisson", "dist_param": {"lam": demand_lam}}),
         (4, 1, {"L": 1, "p": 5.500, "g": 0.010}),
         (4, 2, {"L": 1, "p": 5.500, "g": 0.010}),
         (4, 3, {"L": 1, "p": 5.500, "g": 0.010}),
@@ -70,34 +70,90 @@ def custom_graph(demand_lam=20):
 
 
 MARKET_SAMPLERS = {"poisson": 1, "binomial": 2, "integers": 3, "geometric": 4}
+# the keyword arguments each numpy Generator method takes here (dist_param keys)
+SAMPLER_KWARGS = {"poisson": {"lam"}, "binomial": {"n", "p"}, "integers": {"low", "high"}, "geometric": {"p"}}
+# demand 0 without a draw: numpy's poisson(0) returns 0 and consumes no uniform,
+# which is the reference's `lambda: 0` fallback (network_management.py:264-267)
+ZERO_DEMAND = (1, 0.0, 0, 0, 0.0)
+
+_SKIP_OPS = {"RESUME", "COPY_FREE_VARS", "CACHE", "NOP", "PUSH_NULL", "PRECALL", "MAKE_CELL"}
+
+
+def _lambda_method(f):
+    """The Generator method of ``lambda **p: <receiver>.np_random.<method>(**p)``
+    (network_management.py:125), read from the bytecode; None for any other shape
+    (arithmetic on the draw, another generator, positional arguments, ...)."""
+    import dis
+    import inspect
+    code = getattr(f, "__code__", None)
+    if code is None or code.co_argcount or code.co_kwonlyargcount or code.co_posonlyargcount:
+        return None
+    if not code.co_flags & inspect.CO_VARKEYWORDS or code.co_flags & inspect.CO_VARARGS:
+        return None
+    kw = code.co_varnames[0]
+    ins = [i for i in dis.get_instructions(f) if i.opname not in _SKIP_OPS]
+    if len(ins) < 5:
+        return None
+    recv, attr, meth = ins[:3]
+    if recv.opname not in ("LOAD_DEREF", "LOAD_GLOBAL", "LOAD_FAST", "LOAD_NAME") or recv.argval == kw:
+        return None
+    if attr.opname != "LOAD_ATTR" or attr.argval != "np_random":
+        return None
+    if meth.opname not in ("LOAD_ATTR", "LOAD_METHOD") or meth.argval not in MARKET_SAMPLERS:
+        return None
+    calls = kwloads = 0
+    for i in ins[3:]:
+        if i.opname == "LOAD_FAST" and i.argval == kw:
+            kwloads += 1
+        elif i.opname in ("CALL_FUNCTION_EX",):
+            calls += 1
+        elif not ((i.opname == "LOAD_CONST" and i.argval == ()) or (i.opname == "BUILD_TUPLE" and i.arg == 0)
+                  or (i.opname == "BUILD_MAP" and i.arg == 0) or i.opname in ("DICT_MERGE", "RETURN_VALUE")):
+            return None
+    if calls != 1 or kwloads != 1 or ins[-1].opname != "RETURN_VALUE" or ins[-2].opname != "CALL_FUNCTION_EX":
+        return None
+    return meth.argval
+
+
+def sampler_method(f):
+    """Name of the numpy Generator method a market's ``demand_dist_func`` calls.
+
+    Accepted: a method name (``"poisson"``, the package's own graphs), a bound
+    method of a numpy Generator (``env.np_random.poisson``), or the reference's
+    lambda shape ``lambda **p: self.np_random.poisson(**p)``
+    (network_management.py:125).  The device draws from the env's own stream,
+    as the reference's lambda over ``self.np_random`` does.  Anything else
+    raises: the device cannot run an arbitrary Python callable."""
+    if isinstance(f, str):
+        name = f
+    elif getattr(f, "__self__", None) is not None and type(f.__self__).__name__ == "Generator":
+        name = getattr(f, "__name__", None)
+    else:
+        name = _lambda_method(f)
+    if name not in MARKET_SAMPLERS:
+        raise ValueError(f"unsupported demand_dist_func {f!r}: it must be one of "
+                         f"{sorted(MARKET_SAMPLERS)} by name, a numpy Generator's bound method, or "
+                         f"`lambda **p: <env>.np_random.<method>(**p)`")
+    return name
 
 
 def market_sampler(attrs):
     """Demand source of a market link -> (kind, lam, n_or_low, high, p).
 
-    The reference stores a sampler lambda, `demand_dist_func`, called with
-    `dist_param` (network_management.py:125-127, 257-263): numpy poisson in its
-    own graphs, any np_random method in a user's.  The device runs numpy's
-    poisson, binomial, integers and geometric samplers, so the method is read
-    from `demand_dist_func` -- a method name, or the name the lambda's code
-    references (`lambda **p: self.np_random.binomial(**p)`) -- else from the
-    keys of `dist_param`: {lam} poisson, {n, p} binomial, {low[, high]}
-    integers, {p} geometric.  integers(low, high) draws [low, high), and
-    integers(low) [0, low), as numpy's Generator.integers."""
-    f = attrs.get("demand_dist_func")
-    name = f if isinstance(f, str) else None
-    if name is None and f is not None:
-        hit = set(MARKET_SAMPLERS) & set(getattr(getattr(f, "__code__", None), "co_names", ()))
-        if len(hit) != 1:
-            raise ValueError(f"demand_dist_func must call one of np_random.{sorted(MARKET_SAMPLERS)}")
-        name = hit.pop()
-    dp = dict(attrs.get("dist_param", {}))
-    if name is None:
-        keys = set(dp)
-        name = ("poisson" if keys <= {"lam"} else "binomial" if keys == {"n", "p"} else
-                "integers" if keys in ({"low"}, {"low", "high"}) else "geometric" if keys == {"p"} else None)
-    if name not in MARKET_SAMPLERS:
-        raise ValueError(f"unsupported market demand source: {name!r} with dist_param {dp}")
+    network_management.py:257-267: a market draws only if the edge has both
+    ``demand_dist_func`` and ``dist_param`` (the sampler is called with
+    ``**dist_param``); otherwise its demand is 0 and no draw is made
+    (``ZERO_DEMAND``).  The device runs numpy's poisson, binomial, integers and
+    geometric samplers; ``integers(low, high)`` draws [low, high) and
+    ``integers(low)`` [0, low), as numpy's Generator.integers, and
+    ``poisson()`` without ``lam`` is numpy's default lam=1.0."""
+    if "demand_dist_func" not in attrs or "dist_param" not in attrs:
+        return ZERO_DEMAND
+    name = sampler_method(attrs["demand_dist_func"])
+    dp = dict(attrs["dist_param"])
+    extra = set(dp) - SAMPLER_KWARGS[name]
+    if extra:
+        raise ValueError(f"{name} market demand: unsupported dist_param keys {sorted(extra)}")
     try:
         if name == "poisson":
             return 1, float(dp.get("lam", 1.0)), 0, 0, 0.0
@@ -109,6 +165,78 @@ def market_sampler(attrs):
         return 4, 0.0, 0, 0, float(dp["p"])
     except KeyError as e:
         raise ValueError(f"{name} market demand needs dist_param {e.args[0]!r}") from None
+
+
+def classify(g):
+    """network_management.py:158-181: (market, rawmat, factory, distrib, retail,
+    main_nodes, reorder_links, retail_links, network_links)."""
+    nodes = list(g.nodes())
+    market = [j for j in nodes if not list(g.successors(j))]
+    rawmat = [j for j in nodes if not list(g.predecessors(j))]
+    factory = [j for j in nodes if "C" in g.nodes[j]]
+    distrib = [j for j in nodes if "I0" in g.nodes[j] and "C" not in g.nodes[j] and j not in rawmat]
+    retail = [j for j in distrib if any(s in market for s in g.successors(j))]
+    main = sorted(set(distrib + factory))
+    reorder = sorted(e for e in g.edges() if "L" in g.edges[e])
+    retail_links = [e for e in g.edges() if "L" not in g.edges[e]]
+    network_links = sorted(g.edges())
+    return market, rawmat, factory, distrib, retail, main, reorder, retail_links, network_links
+
+
+def market_demand_attrs(g, e, user_D, sample_path, num_periods):
+    """The (user_D, sample_path) a market link carries after the reference's
+    `_initialize_graph_dependent_attributes` (network_management.py:149-163):
+    an entry of the `user_D` argument overrides the edge's own attribute and
+    brings its `sample_path` entry (default False) with it; a market link with
+    neither gets zeros(num_periods) and False."""
+    if e in user_D:
+        d = user_D[e]
+        return (list(d) if not isinstance(d, (list, np.ndarray)) else d), sample_path.get(e, False)
+    attrs = g.edges[e]
+    d = attrs["user_D"] if "user_D" in attrs else np.zeros(num_periods)
+    return d, attrs.get("sample_path", False)
+
+
+def validate_inputs(g, num_periods, user_D=None, sample_path=None):
+    """network_management.py:197-233, node then edge attribute checks, with the
+    reference's AssertionError messages.  (The scalar checks of :236-238 are the
+    env constructor's.)"""
+    user_D = user_D or {}
+    sample_path = sample_path or {}
+    market, rawmat, factory, distrib, _, main, reorder, retail_links, _ = classify(g)
+    classified = set(market) | set(distrib) | set(factory) | set(rawmat)
+    if set(g.nodes()) != classified:
+        print(f"Warning: Some nodes not classified: {set(g.nodes()) - classified}")
+    for link in user_D:
+        if link not in g.edges:
+            print(f"Warning: Link {link} from user_D not found in graph.")
+    main_s, factory_s, reorder_s, retail_s = set(main), set(factory), set(reorder), set(retail_links)
+    for j in g.nodes():
+        attrs = g.nodes[j]
+        if j in main_s:
+            assert "I0" in attrs and attrs["I0"] >= 0, f"Node {j}: Invalid or missing I0>=0"
+            assert "h" in attrs and attrs["h"] >= 0, f"Node {j}: Invalid or missing h>=0"
+        if j in factory_s:
+            assert "C" in attrs and attrs["C"] > 0, f"Node {j}: Invalid or missing C>0"
+            assert "o" in attrs and attrs["o"] >= 0, f"Node {j}: Invalid or missing o>=0"
+            assert "v" in attrs and 0 < attrs["v"] <= 1, f"Node {j}: Invalid or missing v in (0, 1]"
+    for u, v, attrs in g.edges(data=True):
+        edge = (u, v)
+        if edge in reorder_s:
+            assert "L" in attrs and attrs["L"] >= 0, f"Edge {edge}: Invalid or missing L>=0"
+            assert "p" in attrs and attrs["p"] >= 0, f"Edge {edge}: Invalid or missing p>=0"
+            assert "g" in attrs and attrs["g"] >= 0, f"Edge {edge}: Invalid or missing g>=0"
+        if edge in retail_s:
+            assert "p" in attrs and attrs["p"] >= 0, f"Edge {edge}: Invalid or missing p>=0 (price)"
+            assert "b" in attrs and attrs["b"] >= 0, f"Edge {edge}: Invalid or missing b>=0 (backlog cost)"
+            d, sp = market_demand_attrs(g, edge, user_D, sample_path, num_periods)
+            # every market link carries user_D by now (:159-161), so this never fires
+            assert "demand_dist_func" in attrs or d is not None, \
+                f"Edge {edge}: Missing demand source ('demand_dist_func' or 'user_D')"
+            if "demand_dist_func" in attrs:
+                assert "dist_param" in attrs, f"Edge {edge}: Missing 'dist_param' for 'demand_dist_func'"
+            if np.sum(d) > 0 and not sp:
+                assert len(d) == num_periods, f"Edge {edge}: user_D length {len(d)} != num_periods {num_periods}"
 
 
 @dataclass
@@ -142,19 +270,14 @@ class Topology:
                               int(self.num_periods), int(bool(backlog)), float(alpha), *ptrs)
 
 
-def compile_graph(g, num_periods, user_D=None, sample_path=None):
+def compile_graph(g, num_periods, user_D=None, sample_path=None, validate=True):
+    """Validate (network_management.py:197-233; skipped with validate=False by a
+    caller that already did) and compile a graph to the kernel's tables."""
     user_D = user_D or {}
     sample_path = sample_path or {}
-    nodes = list(g.nodes())
-    market = [j for j in nodes if not list(g.successors(j))]
-    rawmat = [j for j in nodes if not list(g.predecessors(j))]
-    factory = [j for j in nodes if "C" in g.nodes[j]]
-    distrib = [j for j in nodes if "I0" in g.nodes[j] and "C" not in g.nodes[j] and j not in rawmat]
-    retail = [j for j in distrib if any(s in market for s in g.successors(j))]
-    main = sorted(set(distrib + factory))
-    reorder = sorted(e for e in g.edges() if "L" in g.edges[e])
-    retail_links = [e for e in g.edges() if "L" not in g.edges[e]]
-    network_links = sorted(g.edges())
+    if validate:
+        validate_inputs(g, num_periods, user_D, sample_path)
+    market, rawmat, factory, distrib, retail, main, reorder, retail_links, network_links = classify(g)
     mi = {j: i for i, j in enumerate(main)}
     ei = {e: i for i, e in enumerate(reorder)}
     ri = {e: i for i, e in enumerate(retail_links)}
@@ -164,14 +287,15 @@ def compile_graph(g, num_periods, user_D=None, sample_path=None):
     for r, _ in retail_links:
         if r not in mi:
             raise ValueError(f"retail link source {r} must be a main (inventory) node")
-    nattr = lambda j, k, d=0.0: g.nodes[j].get(k, d)  # noqa: E731
+    nattr = lambda j, k: g.nodes[j].get(k, 0.0)  # noqa: E731  (C, o, v only on factories)
     T = int(num_periods)
     t = {
-        "I0": np.array([nattr(j, "I0") for j in main], np.float64),
-        "h": np.array([nattr(j, "h") for j in main], np.float64),
+        "I0": np.array([g.nodes[j]["I0"] for j in main], np.float64),
+        "h": np.array([g.nodes[j]["h"] for j in main], np.float64),
         "C": np.array([nattr(j, "C") for j in main], np.float64),
         "o": np.array([nattr(j, "o") for j in main], np.float64),
-        "v": np.array([nattr(j, "v", 1.0) for j in main], np.float64),
+        # distributors consume order_fulfilled / 1.0 (:484)
+        "v": np.array([g.nodes[j]["v"] if j in factory else 1.0 for j in main], np.float64),
         "is_factory": np.array([j in factory for j in main], np.int32),
         "is_retail": np.array([j in retail for j in main], np.int32),
         "sup": np.array([mi.get(s, -1) if s not in rawmat else -1 for s, _ in reorder], np.int32),
@@ -184,7 +308,7 @@ def compile_graph(g, num_periods, user_D=None, sample_path=None):
         "rl_p": np.array([g.edges[e]["p"] for e in retail_links], np.float64),
         "rl_b": np.array([g.edges[e]["b"] for e in retail_links], np.float64),
     }
-    # demand source per market link (network_management.py:240-267)
+    # demand source per market link (network_management.py:246-267)
     lam = np.zeros(len(retail_links), np.float64)
     use = np.zeros(len(retail_links), np.int32)
     kind = np.ones(max(len(retail_links), 1), np.int32)
@@ -194,16 +318,15 @@ def compile_graph(g, num_periods, user_D=None, sample_path=None):
     uD = np.zeros((max(len(retail_links), 1), T), np.float64)
     for e, r in ri.items():
         attrs = g.edges[e]
-        d = user_D.get(e, attrs.get("user_D"))
-        sp = sample_path.get(e, attrs.get("sample_path", False))
-        if d is not None and np.sum(d) > 0 and not sp:
-            d = np.asarray(d, np.float64)
-            if len(d) != T:
-                raise ValueError(f"Edge {e}: user_D length {len(d)} != num_periods {T}")
-            uD[r] = d
+        d, sp = market_demand_attrs(g, e, user_D, sample_path, T)
+        if np.sum(d) > 0 and not sp:                                   # :250-255
+            uD[r] = np.asarray(d, np.float64)
             use[r] = 1
-        else:
-            kind[r], lam[r], n_lo[r], high[r], prob[r] = market_sampler(attrs)
+        else:                                                          # :257-267
+            src = market_sampler(attrs)
+            if src is ZERO_DEMAND:
+                print(f"Warning: No valid demand source for edge {e}. Defaulting to 0.")
+            kind[r], lam[r], n_lo[r], high[r], prob[r] = src
     t["rl_lam"], t["rl_user"], t["user_D"] = lam, use, uD
     t["rl_dist"], t["rl_n"], t["rl_high"], t["rl_dp"] = kind, n_lo, high, prob
     sp_, sk, sx, pp, px = [0], [], [], [0], []

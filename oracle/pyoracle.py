@@ -322,7 +322,8 @@ class OracleInvMgmt(_Base):
 
 # ---------------------------------------------------------------- NetInvMgmt
 def default_graph():
-    """network_management.py:108-139 default topology (data only; demand Poisson(20))."""
+    """network_management.py:108-139 default topology; the market's
+    `lambda **p: self.np_random.poisson(**p)` (:125) is named by its method."""
     import networkx as nx
     g = nx.DiGraph()
     g.add_nodes_from([0])
@@ -334,7 +335,7 @@ def default_graph():
     g.add_nodes_from([6], I0=380, C=80, o=0.012, v=1.000, h=0.011)
     g.add_nodes_from([7, 8])
     g.add_edges_from([
-        (1, 0, {"p": 2.000, "b": 0.100, "dist_param": {"lam": 20}}),
+        (1, 0, {"p": 2.000, "b": 0.100, "demand_dist_func": "poisson", "dist_param": {"lam": 20}}),
         (2, 1, {"L": 5, "p": 1.500, "g": 0.010}),
         (3, 1, {"L": 3, "p": 1.600, "g": 0.015}),
         (4, 2, {"L": 8, "p": 1.000, "g": 0.008}),
@@ -359,9 +360,9 @@ def custom_graph():
     g.add_nodes_from([5], I0=1200, C=80, o=0.012, v=1.000, h=0.100)
     g.add_nodes_from([6])
     g.add_edges_from([
-        (1, 0, {"p": 25.000, "b": 0.200, "dist_param": {"lam": 20}}),
-        (2, 0, {"p": 25.000, "b": 0.200, "dist_param": {"lam": 20}}),
-        (3, 0, {"p": 25.000, "b": 0.200, "dist_param": {"lam": 20}}),
+        (1, 0, {"p": 25.000, "b": 0.200, "demand_dist_func": "poisson", "dist_param": {"lam": 20}}),
+        (2, 0, {"p": 25.000, "b": 0.200, "demand_dist_func": "poisson", "dist_param": {"lam": 20}}),
+        (3, 0, {"p": 25.000, "b": 0.200, "demand_dist_func": "poisson", "dist_param": {"lam": 20}}),
         (4, 1, {"L": 1, "p": 5.500, "g": 0.010}),
         (4, 2, {"L": 1, "p": 5.500, "g": 0.010}),
         (4, 3, {"L": 1, "p": 5.500, "g": 0.010}),
@@ -371,22 +372,28 @@ def custom_graph():
 
 
 def market_sampler(attrs):
-    """(kind, lam, n_or_low, high, p) of a market link's demand source: the numpy
-    Generator method its `demand_dist_func` calls (a string, or the method name
-    the lambda's code references, as `lambda **p: self.np_random.binomial(**p)`),
-    else the one `dist_param`'s keys name; kind 1 poisson, 2 binomial,
-    3 integers [low, high), 4 geometric (network_management.py:125-127, 257-263)."""
-    f = attrs.get("demand_dist_func")
+    """(kind, lam, n_or_low, high, p) of a market link's demand source
+    (network_management.py:257-267): only an edge with BOTH `demand_dist_func`
+    and `dist_param` draws, `demand_dist_func(**dist_param)`; any other market
+    has demand 0 and makes no draw, which is kind 1 with lam 0 (numpy's
+    poisson(0) returns 0 without consuming a uniform).  The method is a
+    string, a Generator's bound method, or the method name in the reference's
+    lambda (`self.np_random.<method>(**p)`, read from its code names); kind 1
+    poisson (numpy default lam 1.0), 2 binomial, 3 integers [low, high), 4
+    geometric."""
+    if "demand_dist_func" not in attrs or "dist_param" not in attrs:
+        return 1, 0.0, 0, 0, 0.0
+    f = attrs["demand_dist_func"]
     names = {"poisson", "binomial", "integers", "geometric"}
-    name = f if isinstance(f, str) else None
-    if name is None and f is not None:
-        hit = names & set(getattr(getattr(f, "__code__", None), "co_names", ()))
-        name = hit.pop() if len(hit) == 1 else None
-    dp = dict(attrs.get("dist_param", {}))
-    if name is None:
-        keys = set(dp)
-        name = ("poisson" if keys <= {"lam"} else "binomial" if keys == {"n", "p"} else
-                "integers" if keys in ({"low"}, {"low", "high"}) else "geometric" if keys == {"p"} else None)
+    if isinstance(f, str):
+        name = f
+    elif hasattr(f, "__self__"):
+        name = f.__name__
+    else:
+        co = getattr(getattr(f, "__code__", None), "co_names", ())
+        hit = names & set(co)
+        name = hit.pop() if len(hit) == 1 and "np_random" in co else None
+    dp = dict(attrs["dist_param"])
     if name == "poisson":
         return 1, float(dp.get("lam", 1.0)), 0, 0, 0.0
     if name == "binomial":
@@ -399,8 +406,11 @@ def market_sampler(attrs):
     raise ValueError(f"unsupported market demand source {attrs!r}")
 
 
-def net_tables(g, num_periods, user_D=None):
-    """Restates network_management.py:146-195 (node/link classification and ordering)."""
+def net_tables(g, num_periods, user_D=None, sample_path=None):
+    """Restates network_management.py:146-195 (node/link classification and
+    ordering) and the market demand sources of :149-163, :246-267: a link in
+    `user_D` with a positive sum and sample_path False replays it, every other
+    market link takes `market_sampler`."""
     nodes = list(g.nodes())
     market = [j for j in nodes if not list(g.successors(j))]
     rawmat = [j for j in nodes if not list(g.predecessors(j))]
@@ -431,8 +441,7 @@ def net_tables(g, num_periods, user_D=None):
     t["rl_node"] = np.array([mi[r] for r, _ in retail_links], np.int32)
     t["rl_p"] = np.array([g.edges[e]["p"] for e in retail_links], np.float64)
     t["rl_b"] = np.array([g.edges[e]["b"] for e in retail_links], np.float64)
-    ms = [market_sampler(g.edges[e]) if ("dist_param" in g.edges[e] or "demand_dist_func" in g.edges[e])
-          else (1, 0.0, 0, 0, 0.0) for e in retail_links]
+    ms = [market_sampler(g.edges[e]) for e in retail_links]
     t["rl_lam"] = np.array([m[1] for m in ms], np.float64)
     t["rl_dist"] = np.array([m[0] for m in ms] or [1], np.int32)
     t["rl_n"] = np.array([m[2] for m in ms] or [0], np.int64)
@@ -440,10 +449,14 @@ def net_tables(g, num_periods, user_D=None):
     t["rl_dp"] = np.array([m[4] for m in ms] or [0.0], np.float64)
     uD = np.zeros((max(RL, 1), num_periods), np.float64)
     rl_user = np.zeros(max(RL, 1), np.int32)
-    for e, d in (user_D or {}).items():
-        if e in ri and np.sum(d) > 0:
-            uD[ri[e]] = np.asarray(d, np.float64)
-            rl_user[ri[e]] = 1
+    for e, r in ri.items():
+        if e in (user_D or {}):
+            d, sp = user_D[e], (sample_path or {}).get(e, False)
+        else:
+            d, sp = g.edges[e].get("user_D", ()), g.edges[e].get("sample_path", False)
+        if len(d) and np.sum(d) > 0 and not sp:
+            uD[r] = np.asarray(d, np.float64)
+            rl_user[r] = 1
     t["rl_user"], t["user_D"] = rl_user, uD
     sn = np.zeros(J, np.int32)
     sk = np.zeros((J, MAXADJ), np.int32)
@@ -471,11 +484,11 @@ class OracleNet(_Base):
     callers pass the *effective* backlog flag here."""
     fam = "net"
 
-    def __init__(self, n, graph=None, num_periods=30, backlog=True, alpha=1.0, user_D=None):
+    def __init__(self, n, graph=None, num_periods=30, backlog=True, alpha=1.0, user_D=None, sample_path=None):
         if graph is None:
             graph = default_graph()
         self.n = n
-        self.topo = net_tables(graph, num_periods, user_D)
+        self.topo = net_tables(graph, num_periods, user_D, sample_path)
         self._t = {k: np.ascontiguousarray(v) for k, v in self.topo["tables"].items()}
         t = self._t
         self.cfg = NetCfg(self.topo["J"], self.topo["E"], self.topo["RL"], int(num_periods),

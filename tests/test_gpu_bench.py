@@ -52,12 +52,21 @@ def test_bench_single_gpu_line():
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
     # the fused rollout region of the same handle rides along
+    # over whole episode cycles (31 launches x 30 steps = 30 cycles of 31 steps),
+    # so every env finishes exactly 30 episodes in its timed window
     ro = d["rollout"]
-    assert ro["K"] == 30 and ro["steps"] == 300 and ro["value"] > 0
+    assert ro["K"] == 30 and ro["steps"] == 930 and ro["value"] > 0
     assert 0 < ro["roofline"]["frac"] < 1.5
-    # timed steps 5..24: no episode ends, every reward of the region is folded
+    rep = ro["episode_stats"]
+    assert rep["episodes"] == 30 * 65536 and rep["cycles"] == 30
+    assert rep["mean_return"] == rep["mean_return"] and rep["std_return"] > 0
+    # timed steps 5..24: no episode ends (the line says why), every reward of the region is folded
     ep = d["episode_stats"]
-    assert ep["episodes"] == 0 and ep["reward_sum"] != 0
+    assert ep["episodes"] == 0 and ep["reward_sum"] != 0 and "no episode ends" in ep["note"]
+    # the same step loop as graph replays: one 31-step cycle (+ fold) per replay
+    gr = d["graph"]
+    assert gr["steps"] == 31 and gr["replays"] == 1 and gr["value"] > 0
+    assert gr["episode_stats"]["episodes"] == 65536
 
 
 def test_bench_episode_stats_from_timed_batch():

@@ -1287,3 +1287,49 @@ def test_invmgmt_wide_orders_vs_oracle(gpu, oracle, monkeypatch, roll):
         a = acts()
         o, r, _, _, _ = env.step(torch.from_numpy(a).to(gpu))
         check(o.cpu().numpy(), r.cpu().numpy(), a, f"step {12 + 25 + s}")
+
+
+@pytest.mark.parametrize("generic", [False, True])
+def test_net_zero_demand_markets_vs_oracle(gpu, oracle, monkeypatch, generic):
+    """VERDICT r03 item 1 (network_management.py:257-267): on the custom graph,
+    a market with neither demand_dist_func nor dist_param and a market with
+    dist_param only have demand 0 and make no draw; the third market's
+    reference-style lambda draws Poisson(20).  Two episodes (NEXT_STEP reset
+    between them) and a fused rollout, against the oracle: demands, obs and
+    rewards, and every env's final PCG64 state (an extra draw would move it).
+    The specialised custom-graph kernels (lam 0 -> no draw) and the generic
+    table-walking kernel both."""
+    from invsim import NetInvMgmtBacklogEnv
+    from test_topology import _three_market_graph
+    if generic:
+        monkeypatch.setenv("INVSIM_NET_GENERIC", "1")
+    g = _three_market_graph()
+    n = 3000
+    env = NetInvMgmtBacklogEnv(n, device=gpu, graph=g, record_demand=True)
+    assert env.kernel_variant == (0 if generic else 2)
+    orc = oracle.OracleNet(n, graph=g)
+    orc.seed(range(77, 77 + n))
+    assert _eq_bits(env.reset(seed=77)[0].cpu().numpy(), orc.reset())
+    rng = np.random.default_rng(5)
+    for s in range(61):
+        a = rng.uniform(0, 60, size=(n, env.action_dim)).astype(np.float32)
+        o, r, te, tr, info = env.step(torch.from_numpy(a).to(gpu))
+        if s == 30:
+            assert _eq_bits(o.cpu().numpy(), orc.reset())
+            continue
+        e_obs, e_rew, e_tr, e_info = orc.step(a, info=True)
+        dem = info["demand"].cpu().numpy().reshape(e_info["D"].shape)
+        assert not dem[:, :2].any(), f"zero-demand markets drew at step {s}"
+        assert dem[:, 2].mean() > 15
+        assert np.array_equal(dem, e_info["D"].astype(np.int64)), f"demand step {s}"
+        assert _eq_bits(o.cpu().numpy(), e_obs), f"obs step {s}"
+        _assert_reward(r.cpu().numpy(), e_rew, f"step {s}")
+    acts = rng.uniform(0, 60, size=(20, n, env.action_dim)).astype(np.float32)
+    o2, r2, _, _ = env.rollout(torch.from_numpy(acts).to(gpu))
+    assert _eq_bits(o2[0].cpu().numpy(), orc.reset())
+    for k in range(1, 20):
+        e_obs, e_rew, _ = orc.step(acts[k])
+        assert _eq_bits(o2[k].cpu().numpy(), e_obs), f"rollout step {k}"
+        _assert_reward(r2[k].cpu().numpy(), e_rew, f"rollout step {k}")
+    rng_gpu = env.state_fields()["rng"].cpu().numpy().view(np.uint64).T
+    assert np.array_equal(rng_gpu, orc.rng_state())

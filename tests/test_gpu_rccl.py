@@ -1,0 +1,102 @@
+"""RCCL on one GPU: a world-1 "nccl" process group with
+device_id=cuda:0 runs the collectives an 8-GPU node runs -- EpisodeStats'
+all-reduce of device tensors, evaluate_agent's all_gather / all_reduce(MAX) of
+device tensors, and bench.py under torch.distributed.run with the nccl backend
+(init, barriers, max-over-ranks timing, statistics all-reduce) -- and their
+results equal the gloo and no-process-group results exactly."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N_EP, SEED = 777, 21
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _work(invsim, torch):
+    """Episode statistics of 62 steps of 4096 envs (two truncations each) and an
+    evaluate_agent run; returns plain numpy/python results."""
+    from invsim.distributed import EpisodeStats
+    dev = torch.device("cuda", 0)
+    env = invsim.InvManagementBacklogEnv(4096, device=dev, copy=False)
+    env.reset(seed=3)
+    g = torch.Generator(device=dev).manual_seed(2)
+    st = EpisodeStats(4096, "cuda")                       # no index: the current device
+    rew = torch.empty((62, 4096), dtype=torch.float64, device=dev)
+    tr = torch.empty((62, 4096), dtype=torch.bool, device=dev)
+    for k in range(62):
+        a = torch.randint(0, 120, (4096, 3), device=dev, generator=g)
+        _, r, _, t, _ = env.step(a)
+        rew[k].copy_(r)
+        tr[k].copy_(t)
+    st.update_block(rew, None, tr)
+    ep = st.allreduce()
+    ev = invsim.policies.evaluate_agent(invsim.BaseStockAgent(), invsim.InvManagementBacklogEnv,
+                                        n_episodes=N_EP, seed_offset=SEED, device="cuda:0")
+    env.close()
+    return ep, {k: np.asarray(v) for k, v in ev.items() if k not in ("Agent", "Error", "Time")}
+
+
+def _worker(rank, port, backend, out):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "or-gym-inventory_amd"))
+    import invsim
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    ep, cols = _work(invsim, torch)
+    assert dist.get_backend() == backend
+    dist.barrier()
+    dist.destroy_process_group()
+    np.savez(out, ep=json.dumps(ep), **cols)
+
+
+@pytest.mark.parametrize("backend", ["nccl", "gloo"])
+def test_world1_process_group_collectives_equal_single_process(gpu, tmp_path, backend):
+    import torch
+    import invsim
+    out = str(tmp_path / "r.npz")
+    mp.spawn(_worker, args=(_free_port(), backend, out), nprocs=1, join=True)
+    ep, cols = _work(invsim, torch)
+    got = np.load(out)
+    assert json.loads(str(got["ep"])) == pytest.approx(ep, nan_ok=True)
+    assert ep["episodes"] == 2 * 4096
+    for k, v in cols.items():
+        assert np.array_equal(got[k], v, equal_nan=True), k
+
+
+def test_bench_under_torchrun_nccl_one_rank():
+    """bench.py's multi-rank path over RCCL with one rank: nccl process group
+    with device_id, barriers, the max-over-ranks all_reduce and the statistics
+    all-reduce on device tensors."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("INVSIM_BENCH_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "bench.py", "--gpus", "1", "--steps", "62", "--warmup", "5", "--n-envs", "8192", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([x for x in p.stdout.strip().splitlines() if x.startswith("{")][-1])
+    assert d["config"]["backend"] == "nccl" and d["ranks"] == 1 and d["n_gpus"] == 1
+    assert d["episode_stats"]["episodes"] == 2 * 8192
+    assert d["rollout"]["episode_stats"]["episodes"] == 30 * 8192
+    assert d["graph"]["episode_stats"]["episodes"] == 2 * 8192

@@ -260,10 +260,15 @@ def test_oracle_net_market_samplers_vs_numpy(oracle, fn, dp):
     through max(0, int(round(.)))."""
     from invsim.topology import custom_graph
     g = custom_graph()
+
+    class Env:
+        np_random = None
+    self = Env()
     for e in list(g.edges()):
         if "L" not in g.edges[e]:
             g.edges[e]["dist_param"] = dict(dp)
-            g.edges[e]["demand_dist_func"] = (lambda **p: None) if fn == "poisson" else fn
+            # the reference's lambda shape for poisson (:125), a method name otherwise
+            g.edges[e]["demand_dist_func"] = (lambda **p: self.np_random.poisson(**p)) if fn == "poisson" else fn
     n, T = 16, 12
     orc = oracle.OracleNet(n, graph=g, num_periods=T)
     orc.seed(range(100, 100 + n))

@@ -112,7 +112,7 @@ def _two_retailer_graph():
     from invsim.topology import default_graph
     g = default_graph()
     g.add_nodes_from([9], I0=60, h=0.025)
-    g.add_edge(9, 0, p=2.5, b=0.2, dist_param={"lam": 7})
+    g.add_edge(9, 0, p=2.5, b=0.2, demand_dist_func="poisson", dist_param={"lam": 7})
     g.add_edge(3, 9, L=2, p=1.4, g=0.012)
     return g
 

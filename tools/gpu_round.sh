@@ -19,7 +19,7 @@ run() {
     if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $*" >&2; exit $rc; fi
 }
 WLS="invmgmt_backlog invmgmt_lostsales newsvendor net_backlog"
-B="--no-cpu-baseline --no-rollout-line"
+B="--no-cpu-baseline --no-rollout-line --no-graph-line"
 for part in $PARTS; do
   case $part in
   tests)

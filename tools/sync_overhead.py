@@ -75,6 +75,11 @@ def main():
             e1.record(stream)
         if wait in ("sync", "noev", "evpre", "rawev"):
             torch.cuda.synchronize(dev)
+        elif wait == "evsync":                # bench.py --stop event
+            e1.synchronize()
+            el_ev = time.perf_counter() - t0
+            torch.cuda.synchronize(dev)
+            return el_ev * 1e6, e0.elapsed_time(e1) * 1e3
         elif wait == "spin":
             while not e1.query():
                 pass
@@ -92,7 +97,7 @@ def main():
     for _ in range(50):
         region(20, "sync")
     for K in (0, 1, 20, 200):
-        for wait in ("sync", "noev", "evpre", "rawev", "spin"):
+        for wait in ("sync", "noev", "evpre", "rawev", "spin", "evsync"):
             w, k = zip(*[region(K, wait) for _ in range(15)])
             w, k = sorted(w), sorted(k)
             print(f"K={K:5d} wait={wait:6s} wall_us med={w[7]:9.1f} min={w[0]:9.1f}  "
