@@ -37,8 +37,25 @@ constexpr int TB_WAVES = 4096, TB_PROBES = 8;   // probe 7: hardware ids
         if (threadIdx.x == (tid) && blockIdx.x < TB_WAVES)                                     \
             g_tbuf[blockIdx.x * TB_PROBES + (i)] = __builtin_amdgcn_s_memrealtime();           \
     } while (0)
+// per wave of a multi-wave workgroup: row blockIdx.x * waves + wave, lane 0
+#define TPROBE_W(i)                                                                            \
+    do {                                                                                       \
+        const unsigned tw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;                \
+        if ((threadIdx.x & 63) == 0 && tw_ < (unsigned)TB_WAVES)                               \
+            g_tbuf[tw_ * TB_PROBES + (i)] = __builtin_amdgcn_s_memrealtime();                  \
+    } while (0)
+#define TPROBE_W_ID()                                                                          \
+    do {                                                                                       \
+        const unsigned tw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;                \
+        if ((threadIdx.x & 63) == 0 && tw_ < (unsigned)TB_WAVES)                               \
+            g_tbuf[tw_ * TB_PROBES + 7] =                                                      \
+                ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |                 \
+                (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                           \
+    } while (0)
 #define TWAIT() __builtin_amdgcn_s_waitcnt(0)
 #else
+#define TPROBE_W(i) do {} while (0)
+#define TPROBE_W_ID() do {} while (0)
 #define TPROBE_AT(i, tid) do {} while (0)
 #define TPROBE(i) do {} while (0)
 #define TPROBE_ID() do {} while (0)

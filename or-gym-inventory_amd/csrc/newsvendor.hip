@@ -559,7 +559,7 @@ __device__ __forceinline__ int64_t nv_poisson_c(G &g, const PtrsConst &c, const 
 // !PRODUCE the host launches no lookahead workgroups (there is nothing to commit).
 template <int LT, bool HIT, bool PRODUCE, class RG = Pcg>
 __global__ void __launch_bounds__(WAVE)
-nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
+nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla, int xcdpair) {
     extern __shared__ __attribute__((aligned(16))) float nv_tile[];
     const int lane = threadIdx.x;
     const int64_t N = P.cm.N;
@@ -576,7 +576,17 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
         // (bid even: PTRS for lam >= 10 and lam == 0; odd: the multiplication
         // method for 0 < lam < 10), so a wave runs one branch, not both one
         // after the other; a lane works only on the workgroup of its env's branch
-        const int64_t e = (int64_t)(PRODUCE ? bid >> 1 : bid) * WAVE + lane;
+        // PRODUCE: which 64 envs and which branch.  xcdpair: the two workgroups of
+        // a group are 8 apart (blocks of 16 = 8 groups x 2 branches), so both --
+        // and the group's step workgroup, when gla % 8 == 0 -- run on the same XCD
+        // (dispatch is round-robin over the 8) and share its L2 for the rows both
+        // read (state, increment, mu); else adjacent (bid >> 1, bid & 1)
+        int grp = PRODUCE ? bid >> 1 : bid, brn = bid & 1;
+        if (PRODUCE && xcdpair && (bid | 15) < gla) {
+            grp = ((bid >> 4) << 3) + (bid & 7);
+            brn = (bid >> 3) & 1;
+        }
+        const int64_t e = (int64_t)grp * WAVE + lane;
         const bool valid = e < N;
         const int64_t el = valid ? e : N - 1;
         if constexpr (RG::kCounter) {   // the fast stream: the draw of launch step ph_step + 1
@@ -586,7 +596,7 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
             g.set_step(P.cm.ph_step + 1);
             g.sub(0);
             const double mu = P.par[4 * S + el];
-            const bool mult_wg = bid & 1;
+            const bool mult_wg = brn;
             if (!mult_wg) {
                 TableStage ts;
                 ts.dst = lg_l;
@@ -617,7 +627,7 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla) {
             g.inc_hi = P.cm.rng.inc_hi[el];
             g.inc_lo = P.cm.rng.inc_lo[el];
             const double mu = P.par[4 * S + el];
-            const bool mult_wg = bid & 1;
+            const bool mult_wg = brn;
             TableStage ts;
             if (!mult_wg) {
                 ts.dst = lg_l;
@@ -1091,7 +1101,10 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             nv_stream_ph<LT>(P, role, lane, e, el, valid, t_start, K, nxt, lg_l, dbuf, pbuf, kb);
             return;
         }
-    } else if (role < 2) {   // ---- stream waves
+    }
+    TPROBE_W(0);
+    TPROBE_W_ID();
+    if constexpr (!RG::kCounter) if (role < 2) {   // ---- stream waves
         const bool multw = role == 1;
         TableStage ts;
         if (!multw) {
@@ -1108,6 +1121,9 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
         if (!multw) ts.flush(lane);
         bool reset_any = false;
         int t = t_start, cb = 0;
+        int ci = 0;
+        (void)ci;
+        TPROBE_W(1);
         for (int k0 = 0; k0 < K;) {
             int len;
             bool rs;
@@ -1168,6 +1184,10 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             }
 #endif
             double *pb = pbuf + cb * NP * WAVE + lane;
+#ifdef INVSIM_TIMING
+            if (ci < 4) TPROBE_W(2 + ci);
+            ci++;
+#endif
             if (rs && mine) {                      // reset() of the owner: 5 uniforms (:105-111)
                 nv_reset_regs<LT>(P, e, st, nullptr, false);
 #pragma unroll
@@ -1198,6 +1218,8 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 for (int j = 0; j < 5; j++) P.par[j * S + e] = st.par[j];
             }
         }
+        TWAIT();
+        TPROBE_W(6);
         return;
     }
     // ---- dynamics wave
@@ -1224,7 +1246,10 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     double lvl = 0.0;     // CLASSIC_NV / SS: the episode's ppf level, once computed
     bool have = false;
     int kk = 0, cb = 0;
+    int ci = 0;
+    (void)ci;
     nv_wg_sync();   // barrier 0: chunk 0 ready
+    TPROBE_W(1);
     for (int k = 0; k < K; k++) {
         const int64_t oi = (int64_t)k * N + e;
         float act = nact;
@@ -1275,6 +1300,10 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
 #endif
         wave_lds_sync();
         if (++kk == CH || rs || k == K - 1) {      // chunk consumed
+#ifdef INVSIM_TIMING
+            if (ci < 4) TPROBE_W(2 + ci);
+            ci++;
+#endif
             if (k + 1 < K) nv_wg_sync();             // barrier of the next chunk
             kk = 0;
             cb ^= 1;
@@ -1284,6 +1313,15 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
 #pragma unroll
         for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
     }
+    TWAIT();
+    TPROBE_W(6);
+}
+
+// INVSIM_NV_XCD=0 keeps the lookahead workgroups of a group adjacent instead of
+// on one XCD (A/B measurements)
+inline bool nv_xcd_pair_enabled() {
+    const char *v = getenv("INVSIM_NV_XCD");
+    return !(v && v[0] == '0');
 }
 
 // INVSIM_NV_ROLL=0 keeps rollouts on nv_run_kernel (A/B measurements, tests)
@@ -1377,11 +1415,12 @@ hipError_t nv_launch_rg(const NvParams &p, int t_u, const PolicyIO *pol, const S
             const int gla = hit ? (produce ? 2 : (ph ? 0 : 1)) * (int)grid_for(p.cm.N, WAVE) : 0;
             const dim3 grid2(grid.x + gla);
             const int cur = slot;
+            const int xp = nv_xcd_pair_enabled() ? 1 : 0;
 #define S_(X)                                                                                                \
     do {                                                                                                     \
-        if (hit && produce) hipLaunchKernelGGL((nv_step1_kernel<X, true, true, RG>), grid2, block, lds, s, p, t_u, io, cur, gla);  \
-        else if (hit) hipLaunchKernelGGL((nv_step1_kernel<X, true, false, RG>), grid2, block, lds, s, p, t_u, io, cur, gla);       \
-        else hipLaunchKernelGGL((nv_step1_kernel<X, false, true, RG>), grid2, block, lds, s, p, t_u, io, cur, gla);                \
+        if (hit && produce) hipLaunchKernelGGL((nv_step1_kernel<X, true, true, RG>), grid2, block, lds, s, p, t_u, io, cur, gla, xp);  \
+        else if (hit) hipLaunchKernelGGL((nv_step1_kernel<X, true, false, RG>), grid2, block, lds, s, p, t_u, io, cur, gla, xp);       \
+        else hipLaunchKernelGGL((nv_step1_kernel<X, false, true, RG>), grid2, block, lds, s, p, t_u, io, cur, gla, xp);                \
     } while (0)
             NV_LT_SWITCH(S_)
 #undef S_

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round 4, session b: per-wave timelines of the Newsvendor rollout and step
+# (TIMING build), the InvMgmt 32768-env step timeline.
+set -u
+OUT=gpurun_out/r04b
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() { echo "+ $*" >&2; "$@"; rc=$?; if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $*" >&2; exit $rc; fi; }
+export INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so
+run timeout -k 10 120 python tools/timing_nv_roll.py > $OUT/nv_roll_timeline.txt 2>&1
+run timeout -k 10 120 python tools/timing_nv_roll.py > $OUT/nv_roll_timeline.2.txt 2>&1
+run timeout -k 10 120 python tools/timing_nv_step.py > $OUT/nv_step_timeline.txt 2>&1
+echo r04b done
+run timeout -k 10 120 python tools/sync_overhead.py --spin > $OUT/sync_overhead_spin.txt 2>&1
+for w in 5 50 500; do
+  run timeout -k 10 120 python bench.py --steps 20 --warmup $w --no-cpu-baseline --no-rollout-line --no-graph-line > $OUT/bench_w$w.json 2>>$OUT/bench_err.log
+done
+echo r04b2 done
+unset INVSIM_LIB
+B="--workload newsvendor --no-cpu-baseline --no-rollout-line --no-graph-line"
+for i in 1 2; do
+  for x in 1 0; do
+    INVSIM_NV_XCD=$x run timeout -k 10 120 python bench.py $B > $OUT/nv_xcd$x.$i.json 2>>$OUT/bench_err.log
+  done
+done
+for x in 1 0; do
+  INVSIM_NV_XCD=$x run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_xcd$x -o run -- \
+      python bench.py $B --steps 200 --warmup 20 > $OUT/pmc_fetch_xcd$x.log 2>&1
+  INVSIM_NV_XCD=$x run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_xcd$x -o run -- \
+      python bench.py $B --steps 200 --warmup 20 > $OUT/pmc_write_xcd$x.log 2>&1
+done
+echo r04b3 done
