@@ -295,7 +295,8 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
         for bi in range(0, n_calls, calls_per_block):
             nb = min(calls_per_block, n_calls - bi)
             sl = blk[0] & 1
-            stream.wait_event(ev_free[sl])              # this slab's previous fold is done
+            if args.fold == "side":
+                stream.wait_event(ev_free[sl])          # this slab's previous fold is done
             if timed:
                 evs[bi // calls_per_block][0].record(stream)
             for j in range(nb):

@@ -944,9 +944,29 @@ struct NvRoll {
     static constexpr size_t lds() {
         return tile_bytes() + RHS_LDS_MAX * sizeof(double) + 2 * (size_t)CH * WAVE * sizeof(int64_t) +
                2 * NP * (size_t)WAVE * sizeof(double) + (size_t)WAVE * sizeof(double) +
-               4 * (JUMP_MAX + 1) * sizeof(uint64_t) + 2 * 2 * (size_t)WAVE * sizeof(uint64_t);
+               4 * (JUMP_MAX + 1) * sizeof(uint64_t) + 2 * 2 * (size_t)WAVE * sizeof(uint64_t) +
+               2 * (size_t)CH * WAVE * sizeof(float);
     }
 };
+
+// The actions of one chunk (launch steps k0 .. k0 + len - 1) into the LDS ring
+// abuf [CH][WAVE] of the chunk, by a stream wave, with LDS-DMA loads
+// (global_load_lds_dword: row j lands at abuf + j * WAVE, lane l at + 4 l)
+// issued at the start of its chunk; nv_wait_actions (vmcnt) before the chunk's
+// barrier, so the loads' latency overlaps the chunk's draws.  That wave issues
+// no global stores, so the wait waits for nothing else, and the dynamics wave
+// has no global load in its loop: a load there made every step wait for the
+// previous step's stores (vmcnt counts stores too, and the compiler's wait at
+// the loop latch was vmcnt(0)).
+__device__ __forceinline__ void nv_load_actions(const StepIO<float, float> &io, int k0, int len, int64_t N,
+                                                int64_t el, float *ab) {
+#pragma unroll
+    for (int j = 0; j < NV_ROLL_CH; j++)
+        if (j < len)
+            __builtin_amdgcn_global_load_lds((const void *)(io.act + (int64_t)(k0 + j) * N + el),
+                                             (__attribute__((address_space(3))) void *)(ab + j * WAVE), 4, 0, 0);
+}
+__device__ __forceinline__ void nv_wait_actions() { __builtin_amdgcn_s_waitcnt(0); }
 
 // The two stream waves of nv_roll_kernel on the fast stream.  A draw is a
 // function of (key, launch step, mu) only -- no generator state, no order
@@ -962,7 +982,8 @@ struct NvRoll {
 template <int LT>
 __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int lane, int64_t e, int64_t el, bool valid,
                                              int t_start, int K, bool nxt, double *lg_l, int64_t *dbuf,
-                                             double *pbuf, uint64_t *kb) {
+                                             double *pbuf, uint64_t *kb, const StepIO<float, float> &io,
+                                             float *abuf, bool stage) {
     constexpr int CH = NvRoll<LT>::CH, NP = NvRoll<LT>::NP;
     const int64_t S = P.cm.Npad;
     {   // both waves draw PTRS candidates: each writes the whole (identical) table
@@ -985,6 +1006,7 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
         const int nd = len - (rs ? 1 : 0);                   // the reset step draws none
         int64_t *dcol = dbuf + cb * CH * WAVE;
         const uint64_t ph0 = P.cm.ph_step + (uint64_t)k0;    // launch step of the chunk's first step
+        if (stage && role == 1) nv_load_actions(io, k0, len, P.cm.N, el, abuf + cb * CH * WAVE);
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
         for (int j = role; j < nd; j += 2) dcol[j * WAVE + lane] = 20;
 #else
@@ -1040,6 +1062,7 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
             }
         }
 #endif
+        if (stage && role == 1) nv_wait_actions();
         double *pb = pbuf + cb * NP * WAVE + lane;
         if (rs && role == 0) {                                // reset() at launch step k0 + len - 1
             st.g.set_step(ph0 + (uint64_t)(len - 1));
@@ -1085,6 +1108,8 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     double *ubuf = pbuf + 2 * NP * WAVE;                                   // [WAVE] mult wave's uniforms
     uint64_t *jt = reinterpret_cast<uint64_t *>(ubuf + WAVE);              // [4][JUMP_MAX + 1] jump table
     uint64_t *kb = jt + 4 * (JUMP_MAX + 1);                                // [2][2][WAVE] fast stream: keys, rates
+    float *abuf = reinterpret_cast<float *>(kb + 2 * 2 * WAVE);            // [2][CH][WAVE] staged actions
+    constexpr bool stage = !POL;                                          // actions through LDS
     const int lane = threadIdx.x & (WAVE - 1);
     const int role = threadIdx.x / WAVE;
     const int64_t N = P.cm.N;
@@ -1098,7 +1123,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     const bool nxt = P.cm.autoreset == AR_NEXT_STEP;
     if constexpr (RG::kCounter) {
         if (role < 2) {   // ---- the fast stream's two stream waves
-            nv_stream_ph<LT>(P, role, lane, e, el, valid, t_start, K, nxt, lg_l, dbuf, pbuf, kb);
+            nv_stream_ph<LT>(P, role, lane, e, el, valid, t_start, K, nxt, lg_l, dbuf, pbuf, kb, io, abuf, stage);
             return;
         }
     }
@@ -1130,6 +1155,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             nv_chunk(t, K - k0, P.step_limit, nxt, CH, len, rs);
             const int nd = mine ? len - (rs ? 1 : 0) : 0;    // draws of this lane (the reset step draws none)
             int64_t *db = dbuf + cb * CH * WAVE + lane;
+            if (stage && multw) nv_load_actions(io, k0, len, N, el, abuf + cb * CH * WAVE);
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
             for (int j = 0; j < nd; j++) db[j * WAVE] = 20;
 #else
@@ -1183,6 +1209,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 }
             }
 #endif
+            if (stage && multw) nv_wait_actions();
             double *pb = pbuf + cb * NP * WAVE + lane;
 #ifdef INVSIM_TIMING
             if (ci < 4) TPROBE_W(2 + ci);
@@ -1238,7 +1265,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             if (!(p >= LT - sc)) st.pv[p] = 0.f;
         }
     }
-    float nact = POL ? 0.f : io.act[el];
+    float nact = 0.f;
     constexpr int MD = 2;                       // metrics: reward sum, steps
     double met[MD];
 #pragma unroll
@@ -1253,7 +1280,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     for (int k = 0; k < K; k++) {
         const int64_t oi = (int64_t)k * N + e;
         float act = nact;
-        if (!POL && k + 1 < K) nact = io.act[(int64_t)(k + 1) * N + el];   // the next step's action
+        if (stage) act = abuf[(cb * CH + kk) * WAVE + lane];       // staged by the mult stream wave
         const bool rs = nxt && sc >= P.step_limit;
         if (rs) {                                                  // NEXT_STEP autoreset
 #pragma unroll
