@@ -942,9 +942,9 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
 // Same arithmetic, in the same order, as im_step_regs.
 // The demand wave of the rollout kernels (stream_flat_loop): Poisson demand
 // (:280) of each launch step into the ring dbuf [RD * CH][WAVE], nb barriers
-template <int CH, int RD, class RG>
+template <int CH, int RD, class RG, class Stage = NoStage>
 __device__ __forceinline__ void im_stream_loop(const ImParams &P, RG &g, const double *rhs_l, int64_t *dbuf,
-                                               int lane, int K, int nb, int t_start) {
+                                               int lane, int K, int nb, int t_start, Stage stage = Stage()) {
     StreamPos<RG> pos(P.cm.ph_step);
     stream_flat_loop<CH, RD, 1>(
         K, nb, t_start, P.periods,
@@ -957,8 +957,39 @@ __device__ __forceinline__ void im_stream_loop(const ImParams &P, RG &g, const d
             return np_poisson_try(g, P.pc, rhs_l, d);
 #endif
         },
-        [&](int slot, int, int64_t d) { dbuf[slot * WAVE + lane] = d < 0 ? 0 : d; });
+        [&](int slot, int, int64_t d) { dbuf[slot * WAVE + lane] = d < 0 ? 0 : d; }, stage);
 }
+
+// The open-loop rollout's actions of chunk b, staged into the LDS ring
+// act_l [2][CH][2 * M1][WAVE] (32-bit halves) by the demand wave with LDS-DMA
+// loads (global_load_lds_dword: row q of step kk lands at + q * WAVE, lane l at
+// + 4 l): chunk b is read by the dynamics wave between barriers b and b + 1, and
+// its buffer (b & 1) was last read before barrier b - 1.
+template <int CH, int M1>
+struct ImActStage {
+    const int64_t *act;
+    uint32_t *act_l;
+    int64_t N, el;
+    int K, nch;
+    __device__ __forceinline__ void operator()(int b) const {
+        if (b >= nch) return;
+#pragma unroll
+        for (int kk = 0; kk < CH; kk++) {
+            const int k = b * CH + kk;
+            if (k < K) {
+                const uint32_t *src = reinterpret_cast<const uint32_t *>(act + ((int64_t)k * N + el) * M1);
+#pragma unroll
+                for (int q = 0; q < 2 * M1; q++)
+                    __builtin_amdgcn_global_load_lds(
+                        (const void *)(src + q),
+                        (__attribute__((address_space(3))) void *)(act_l + (((b & 1) * CH + kk) * 2 * M1 + q) * WAVE),
+                        4, 0, 0);
+            }
+        }
+    }
+    __device__ __forceinline__ void wait() const { __builtin_amdgcn_s_waitcnt(0); }
+};
+constexpr int IM_AP_LDS = 256;   // alpha**t LDS table of the 3-role rollout (periods <= this)
 
 template <int L0, int L1, int L2>
 struct ImLt3 {
@@ -1300,9 +1331,12 @@ struct ImLt3o : ImLt3<L0, L1, L2> {
     static constexpr int CH = IM_ROLL3O_CH;                              // chunk (launch steps)
     static constexpr int RD = IM_ROLL3O_RD;                              // demand ring depth (chunks)
     static constexpr int M1 = 3, O = ImLt3<L0, L1, L2>::O;
-    // POL adds abuf [2][CH][M1][WAVE]: the agent's orders, dynamics -> obs wave
-    static constexpr size_t lds(bool pol = false) {
-        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + (pol ? 4 : 2) * CH * M1 * WAVE * 8;
+    // tile, RHS table, demand ring, ibuf [2][CH][M1][WAVE] (inventory, dynamics ->
+    // obs wave), abuf [2][CH][M1][WAVE] (requested orders, dynamics -> obs wave),
+    // act_l [2][CH][2 M1][WAVE] u32 (actions, demand -> dynamics wave), alpha**t
+    static constexpr size_t lds(bool = false) {
+        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + 4 * CH * M1 * WAVE * 8 +
+               (size_t)2 * CH * 2 * M1 * WAVE * 4 + IM_AP_LDS * 8;
     }
 };
 
@@ -1329,7 +1363,9 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
     double *rhs_l = reinterpret_cast<double *>(im_tile + WAVE * O);
     int64_t *dbuf = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);   // [RD * CH][WAVE]
     int64_t *ibuf = dbuf + G::RD * CH * WAVE;                             // [2][CH][M1][WAVE]
-    int64_t *abuf = ibuf + 2 * CH * M1 * WAVE;                            // POL: [2][CH][M1][WAVE]
+    int64_t *abuf = ibuf + 2 * CH * M1 * WAVE;                            // [2][CH][M1][WAVE]
+    uint32_t *act_l = reinterpret_cast<uint32_t *>(abuf + 2 * CH * M1 * WAVE);   // [2][CH][2 M1][WAVE]
+    double *ap_l = reinterpret_cast<double *>(act_l + 2 * CH * 2 * M1 * WAVE);   // alpha**t, t < periods
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t N = P.cm.N;
     const int64_t S = P.cm.Npad;
@@ -1352,9 +1388,15 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
         }
         RG g;
         P.cm.rng.load(el, g);
+        for (int q = lane; q < P.periods; q += WAVE) ap_l[q] = P.alpha_pow[q];   // before barrier 0
         ts.flush(lane);
         // barriers 0 .. nch - 1 (demand chunk c ready), nch (the obs wave's last chunk)
-        im_stream_loop<CH, G::RD>(P, g, rhs_l, dbuf, lane, K, nch + 1, t_start);
+        if (POL) {
+            im_stream_loop<CH, G::RD>(P, g, rhs_l, dbuf, lane, K, nch + 1, t_start);
+        } else {
+            const ImActStage<CH, M1> stage{io.act, act_l, N, el, K, nch};
+            im_stream_loop<CH, G::RD>(P, g, rhs_l, dbuf, lane, K, nch + 1, t_start, stage);
+        }
         if (valid) P.cm.rng.store_state(e, g);
         return;
     }
@@ -1373,9 +1415,6 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
                 if (v == IM_WIDE) wv[a][i] = P.alog[base + i];
             }
         }
-        int64_t nact[M1];
-#pragma unroll
-        for (int i = 0; i < M1; i++) nact[i] = POL ? 0 : io.act[el * M1 + i];
         wg_lds_sync();   // barrier 0
         for (int c = 0; c < nch; c++) {
             wg_lds_sync();   // barrier c + 1: inventory chunk c ready
@@ -1383,13 +1422,9 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
             const int64_t *ab = abuf + (c & 1) * CH * M1 * WAVE;
             for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
                 const int k = c * CH + kk;
-                int64_t req[M1];
+                int64_t req[M1];   // the step's requested orders, handed over by the dynamics wave
 #pragma unroll
-                for (int i = 0; i < M1; i++) req[i] = POL ? ab[(kk * M1 + i) * WAVE + lane] : nact[i];
-                if (!POL && k + 1 < K) {               // the next step's actions
-#pragma unroll
-                    for (int i = 0; i < M1; i++) nact[i] = io.act[((int64_t)(k + 1) * N + el) * M1 + i];
-                }
+                for (int i = 0; i < M1; i++) req[i] = ab[(kk * M1 + i) * WAVE + lane];
                 if (t >= P.periods) {                  // NEXT_STEP autoreset: [I0, 0...] (:220)
 #pragma unroll
                     for (int q = 0; q < O; q++) trow[q] = (q < M1) ? ib[(kk * M1 + q) * WAVE + lane] : 0;
@@ -1461,9 +1496,6 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
             rw[i][a] = L > 0 ? P.Rring[(int64_t)(P.ring_off[i] + (int)((uint32_t)(t + a) % (uint32_t)L)) * S + el] : 0;
         }
     }
-    int64_t nact[M1];
-#pragma unroll
-    for (int i = 0; i < M1; i++) nact[i] = POL ? 0 : io.act[el * M1 + i];
     // POL: hv[i][a] = action_log[t - 1 - a, i], the last W(i) requested orders of stage i
     int64_t hv[M1][D > 0 ? D : 1];
 #pragma unroll
@@ -1476,29 +1508,24 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
     double met[MD];
 #pragma unroll
     for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
-    double napow = P.alpha_pow[t < P.periods ? t : 0];   // alpha**t of the next step, prefetched
     int64_t dlast = 0;
     bool last_real = false;
-    wg_lds_sync();   // barrier 0: demand chunk 0 ready
+    wg_lds_sync();   // barrier 0: demand chunk 0 (and its actions, alpha**t) ready
     for (int c = 0; c < nch; c++) {
         const int64_t *db = dbuf + (c % G::RD) * CH * WAVE;
         int64_t *ib = ibuf + (c & 1) * CH * M1 * WAVE;
         int64_t *ab = abuf + (c & 1) * CH * M1 * WAVE;
+        const uint32_t *al = act_l + (c & 1) * CH * 2 * M1 * WAVE;
         for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
             const int k = c * CH + kk;
             const int64_t oi = (int64_t)k * N + e;
             int64_t req[M1];
 #pragma unroll
-            for (int i = 0; i < M1; i++) req[i] = nact[i];
-            const double apow = napow;
-            {
-                const int tn = (t >= P.periods) ? 0 : t + 1;     // the next launch step's period
-                napow = P.alpha_pow[tn < P.periods ? tn : 0];
-            }
-            if (!POL && k + 1 < K) {               // prefetch the next step's actions
-#pragma unroll
-                for (int i = 0; i < M1; i++) nact[i] = io.act[((int64_t)(k + 1) * N + el) * M1 + i];
-            }
+            for (int i = 0; i < M1; i++)
+                req[i] = POL ? 0
+                             : (int64_t)((uint64_t)al[(kk * 2 * M1 + 2 * i) * WAVE + lane] |
+                                         ((uint64_t)al[(kk * 2 * M1 + 2 * i + 1) * WAVE + lane] << 32));
+            const double apow = ap_l[t < P.periods ? t : 0];
             if (t >= P.periods) {                  // NEXT_STEP autoreset (:197-220)
 #pragma unroll
                 for (int i = 0; i < M1; i++) I[i] = P.I0[i];
@@ -1590,12 +1617,13 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
                     met[1] += 1.0;                                              // episode_steps
 #pragma unroll
                     for (int i = 0; i < M1; i++) {
-                        ab[(kk * M1 + i) * WAVE + lane] = req[i];               // the order -> obs wave
 #pragma unroll
                         for (int a = G::W(i) - 1; a >= 1; a--) hv[i][a] = hv[i][a - 1];
                         hv[i][0] = req[i];
                     }
                 }
+#pragma unroll
+                for (int i = 0; i < M1; i++) ab[(kk * M1 + i) * WAVE + lane] = req[i];   // the order -> obs wave
 #pragma unroll
                 for (int i = 0; i < M1; i++) ib[(kk * M1 + i) * WAVE + lane] = Icur[i];   // obs I (:366)
                 // the new fulfilled-order ring slots R[t] (:267)
@@ -1735,7 +1763,7 @@ hipError_t im_roll_launch(const ImParams &p, bool backlog, int t_u, const Policy
     // wave's chain is the step time, so split it (measured on MI355X:
     // LostSales 32768 envs 87.5 -> 77.7 us per K = 30; at 65536 the
     // 2-role kernel is faster, 118 vs 152 us)
-    const bool three = p.cm.N <= im_roll3o_max_n();
+    const bool three = p.cm.N <= im_roll3o_max_n() && p.periods <= IM_AP_LDS;   // alpha**t table in LDS
     // two groups per workgroup when the group count is even (every workgroup full)
     const bool two = three && im_roll3o_g2(pol != nullptr) && (g3.x % 2) == 0;
     const dim3 g6(g3.x / 2);

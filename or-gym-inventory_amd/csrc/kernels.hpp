@@ -342,14 +342,30 @@ __device__ __forceinline__ bool np_poisson_try(G &g, const PtrsConst &c, const d
 // the consumer is done with the slot's previous step j - RD*CH (barrier
 // (j / CH - RD) + 1 passed).  A NEXT_STEP reset step (t >= T) draws nothing.
 //   draw(j, r, k) -> bool: one attempt for draw r of launch step j; put(slot, r, k): store it
-template <int CH, int RD, int RL, class Draw, class Put>
-__device__ __forceinline__ void stream_flat_loop(int K, int nb, int t, int T, Draw draw, Put put) {
+// A stream wave can also stage other per-step inputs of chunk b for the
+// consumer waves (stage(b), e.g. LDS-DMA loads of the actions): issued when the
+// wave starts chunk b (right after barrier b - 1), waited for (stage.wait())
+// before barrier b.  The stream wave issues no global stores, so that wait
+// waits for nothing else; the consumers then load nothing from global memory in
+// their loops, where a load would wait for their own earlier stores (vmcnt
+// counts stores, and completes in order).
+struct NoStage {
+    __device__ __forceinline__ void operator()(int) const {}
+    __device__ __forceinline__ void wait() const {}
+};
+
+template <int CH, int RD, int RL, class Draw, class Put, class Stage = NoStage>
+__device__ __forceinline__ void stream_flat_loop(int K, int nb, int t, int T, Draw draw, Put put,
+                                                 Stage stage = Stage()) {
     static_assert(RD >= 2, "the ring needs two chunks");
     int j = 0, r = 0, b = 0;
+    stage(0);
     for (;;) {
         while (b < nb && __all(j >= min((b + 1) * CH, K))) {
+            stage.wait();
             roll_wg_sync();                        // barrier b: chunk b drawn
             b++;
+            stage(b);
         }
         if (b == nb) break;
         if (j < K && j / CH - RD + 2 <= b) {

@@ -17,6 +17,15 @@ for i in 1 2; do
   run timeout -k 10 120 python bench.py $R > $OUT/nv_roll_stage.$i.json 2>>$OUT/bench_err.log
   INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_NOSTAGE.so run timeout -k 10 120 python bench.py $R > $OUT/nv_roll_nostage.$i.json 2>>$OUT/bench_err.log
 done
+for w in invmgmt_lostsales; do
+  for m in rollout policy; do
+    R="--workload $w --mode $m --steps 1200 --warmup 60 --no-cpu-baseline"
+    for i in 1 2; do
+      run timeout -k 10 120 python bench.py $R > $OUT/${w}_${m}_stage.$i.json 2>>$OUT/bench_err.log
+      INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_NOSTAGE.so run timeout -k 10 120 python bench.py $R > $OUT/${w}_${m}_nostage.$i.json 2>>$OUT/bench_err.log
+    done
+  done
+done
 B="--workload newsvendor --no-cpu-baseline --no-rollout-line --no-graph-line"
 for i in 1 2; do
   for x in 1 0; do
