@@ -144,6 +144,7 @@ struct NetParams {
     const double *user_D;        // [RL][T]
     const int32_t *succ_ptr, *succ_kind, *succ_idx, *pred_ptr, *pred_idx;
     const double *alpha_pow;     // [T]
+    int32_t rhs_nk_max;          // host: the longest PTRS RHS table of a market (0: none)
     // state
     double *X;                   // [J][Npad]
     double *U;                   // [RL][Npad]

@@ -17,7 +17,7 @@ for i in 1 2; do
   run timeout -k 10 120 python bench.py $R > $OUT/nv_roll_stage.$i.json 2>>$OUT/bench_err.log
   INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_NOSTAGE.so run timeout -k 10 120 python bench.py $R > $OUT/nv_roll_nostage.$i.json 2>>$OUT/bench_err.log
 done
-for w in invmgmt_lostsales; do
+for w in invmgmt_lostsales net_backlog; do
   for m in rollout policy; do
     R="--workload $w --mode $m --steps 1200 --warmup 60 --no-cpu-baseline"
     for i in 1 2; do
