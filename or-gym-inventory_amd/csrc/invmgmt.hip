@@ -990,6 +990,12 @@ struct ImActStage {
     __device__ __forceinline__ void wait() const { __builtin_amdgcn_s_waitcnt(0); }
 };
 constexpr int IM_AP_LDS = 256;   // alpha**t LDS table of the 3-role rollout (periods <= this)
+// Open-loop actions staged by the demand wave (1) or loaded by the dynamics and
+// obs waves themselves (0, the default: LostSales 32 768 envs, 30-step
+// launches, 63.1-64.1 us against 64.9-65.5 staged, profiles/r04/stage_ab)
+#ifndef IM_ROLL3O_STAGE
+#define IM_ROLL3O_STAGE 0
+#endif
 
 template <int L0, int L1, int L2>
 struct ImLt3 {
@@ -1391,7 +1397,7 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
         for (int q = lane; q < P.periods; q += WAVE) ap_l[q] = P.alpha_pow[q];   // before barrier 0
         ts.flush(lane);
         // barriers 0 .. nch - 1 (demand chunk c ready), nch (the obs wave's last chunk)
-        if (POL) {
+        if (POL || !IM_ROLL3O_STAGE) {
             im_stream_loop<CH, G::RD>(P, g, rhs_l, dbuf, lane, K, nch + 1, t_start);
         } else {
             const ImActStage<CH, M1> stage{io.act, act_l, N, el, K, nch};
@@ -1415,6 +1421,10 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
                 if (v == IM_WIDE) wv[a][i] = P.alog[base + i];
             }
         }
+        constexpr bool HANDED = POL || IM_ROLL3O_STAGE;   // requested orders from the dynamics wave
+        int64_t nact[M1];
+#pragma unroll
+        for (int i = 0; i < M1; i++) nact[i] = HANDED ? 0 : io.act[el * M1 + i];
         wg_lds_sync();   // barrier 0
         for (int c = 0; c < nch; c++) {
             wg_lds_sync();   // barrier c + 1: inventory chunk c ready
@@ -1422,9 +1432,13 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
             const int64_t *ab = abuf + (c & 1) * CH * M1 * WAVE;
             for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
                 const int k = c * CH + kk;
-                int64_t req[M1];   // the step's requested orders, handed over by the dynamics wave
+                int64_t req[M1];
 #pragma unroll
-                for (int i = 0; i < M1; i++) req[i] = ab[(kk * M1 + i) * WAVE + lane];
+                for (int i = 0; i < M1; i++) req[i] = HANDED ? ab[(kk * M1 + i) * WAVE + lane] : nact[i];
+                if (!HANDED && k + 1 < K) {            // the next step's actions
+#pragma unroll
+                    for (int i = 0; i < M1; i++) nact[i] = io.act[((int64_t)(k + 1) * N + el) * M1 + i];
+                }
                 if (t >= P.periods) {                  // NEXT_STEP autoreset: [I0, 0...] (:220)
 #pragma unroll
                     for (int q = 0; q < O; q++) trow[q] = (q < M1) ? ib[(kk * M1 + q) * WAVE + lane] : 0;
@@ -1508,9 +1522,13 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
     double met[MD];
 #pragma unroll
     for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
+    constexpr bool STAGED = !POL && IM_ROLL3O_STAGE;
+    int64_t nact[M1];
+#pragma unroll
+    for (int i = 0; i < M1; i++) nact[i] = (POL || STAGED) ? 0 : io.act[el * M1 + i];
     int64_t dlast = 0;
     bool last_real = false;
-    wg_lds_sync();   // barrier 0: demand chunk 0 (and its actions, alpha**t) ready
+    wg_lds_sync();   // barrier 0: demand chunk 0 (and its actions when staged, alpha**t) ready
     for (int c = 0; c < nch; c++) {
         const int64_t *db = dbuf + (c % G::RD) * CH * WAVE;
         int64_t *ib = ibuf + (c & 1) * CH * M1 * WAVE;
@@ -1522,9 +1540,13 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
             int64_t req[M1];
 #pragma unroll
             for (int i = 0; i < M1; i++)
-                req[i] = POL ? 0
-                             : (int64_t)((uint64_t)al[(kk * 2 * M1 + 2 * i) * WAVE + lane] |
-                                         ((uint64_t)al[(kk * 2 * M1 + 2 * i + 1) * WAVE + lane] << 32));
+                req[i] = !STAGED ? nact[i]
+                                 : (int64_t)((uint64_t)al[(kk * 2 * M1 + 2 * i) * WAVE + lane] |
+                                             ((uint64_t)al[(kk * 2 * M1 + 2 * i + 1) * WAVE + lane] << 32));
+            if (!POL && !STAGED && k + 1 < K) {    // prefetch the next step's actions
+#pragma unroll
+                for (int i = 0; i < M1; i++) nact[i] = io.act[((int64_t)(k + 1) * N + el) * M1 + i];
+            }
             const double apow = ap_l[t < P.periods ? t : 0];
             if (t >= P.periods) {                  // NEXT_STEP autoreset (:197-220)
 #pragma unroll
@@ -1622,8 +1644,10 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
                         hv[i][0] = req[i];
                     }
                 }
+                if (POL || STAGED) {
 #pragma unroll
-                for (int i = 0; i < M1; i++) ab[(kk * M1 + i) * WAVE + lane] = req[i];   // the order -> obs wave
+                    for (int i = 0; i < M1; i++) ab[(kk * M1 + i) * WAVE + lane] = req[i];   // the order -> obs wave
+                }
 #pragma unroll
                 for (int i = 0; i < M1; i++) ib[(kk * M1 + i) * WAVE + lane] = Icur[i];   // obs I (:366)
                 // the new fulfilled-order ring slots R[t] (:267)
