@@ -315,7 +315,7 @@ template <int LT, class G = Pcg>
 __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool valid, int sc, NvState<LT, G> &s,
                                              float action, float *orow, const double *lg_l, TableStage *ts,
                                              double &reward, int64_t *dem, int64_t dpre = -1,
-                                             double *irec = nullptr) {
+                                             double *irec = nullptr, bool ring_store = true) {
     const int64_t S = P.cm.Npad;
     const int L = (LT >= 0) ? LT : P.L;
     const int base = (L > 0) ? (int)((uint32_t)(sc + 1) % (uint32_t)L) : 0;  // slot of position 0
@@ -357,7 +357,7 @@ __device__ __forceinline__ bool nv_step_regs(const NvParams &P, int64_t e, bool 
         for (int p = 0; p + 1 < L; p++) orow[5 + p] = pos(p + 1);
         if (L > 0) orow[5 + L - 1] = qf;
     }
-    if (L > 0 && valid) P.pipe[(int64_t)base * S + e] = qf;                // replaces the arrived slot
+    if (L > 0 && valid && ring_store) P.pipe[(int64_t)base * S + e] = qf;  // replaces the arrived slot
     if (LT > 0) {
 #pragma unroll
         for (int p = 0; p + 1 < (LT > 0 ? LT : 1); p++) s.pv[p] = s.pv[p + 1];
@@ -941,32 +941,17 @@ struct NvRoll {
     static constexpr int O = LT + 5;
     static constexpr int NP = 7;   // reset handoff: price, cost, h, k, mu, state hi, state lo
     static constexpr size_t tile_bytes() { return (size_t)((EPW * O + 3) / 4) * 4 * sizeof(float); }
+    // tile, loggam table, demand chunks, reset handoff, mult uniforms, jump table,
+    // fast-stream task table, then the dynamics -> obs handoff: the new order
+    // hq [2][CH][WAVE] f32, the reward hr [2][CH][WAVE] f64, a reset's params
+    // hp [2][5][WAVE] f32
     static constexpr size_t lds() {
         return tile_bytes() + RHS_LDS_MAX * sizeof(double) + 2 * (size_t)CH * WAVE * sizeof(int64_t) +
                2 * NP * (size_t)WAVE * sizeof(double) + (size_t)WAVE * sizeof(double) +
                4 * (JUMP_MAX + 1) * sizeof(uint64_t) + 2 * 2 * (size_t)WAVE * sizeof(uint64_t) +
-               2 * (size_t)CH * WAVE * sizeof(float);
+               2 * (size_t)CH * WAVE * (sizeof(float) + sizeof(double)) + 2 * 5 * (size_t)WAVE * sizeof(float);
     }
 };
-
-// The actions of one chunk (launch steps k0 .. k0 + len - 1) into the LDS ring
-// abuf [CH][WAVE] of the chunk, by a stream wave, with LDS-DMA loads
-// (global_load_lds_dword: row j lands at abuf + j * WAVE, lane l at + 4 l)
-// issued at the start of its chunk; nv_wait_actions (vmcnt) before the chunk's
-// barrier, so the loads' latency overlaps the chunk's draws.  That wave issues
-// no global stores, so the wait waits for nothing else, and the dynamics wave
-// has no global load in its loop: a load there made every step wait for the
-// previous step's stores (vmcnt counts stores too, and the compiler's wait at
-// the loop latch was vmcnt(0)).
-__device__ __forceinline__ void nv_load_actions(const StepIO<float, float> &io, int k0, int len, int64_t N,
-                                                int64_t el, float *ab) {
-#pragma unroll
-    for (int j = 0; j < NV_ROLL_CH; j++)
-        if (j < len)
-            __builtin_amdgcn_global_load_lds((const void *)(io.act + (int64_t)(k0 + j) * N + el),
-                                             (__attribute__((address_space(3))) void *)(ab + j * WAVE), 4, 0, 0);
-}
-__device__ __forceinline__ void nv_wait_actions() { __builtin_amdgcn_s_waitcnt(0); }
 
 // The two stream waves of nv_roll_kernel on the fast stream.  A draw is a
 // function of (key, launch step, mu) only -- no generator state, no order
@@ -982,8 +967,7 @@ __device__ __forceinline__ void nv_wait_actions() { __builtin_amdgcn_s_waitcnt(0
 template <int LT>
 __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int lane, int64_t e, int64_t el, bool valid,
                                              int t_start, int K, bool nxt, double *lg_l, int64_t *dbuf,
-                                             double *pbuf, uint64_t *kb, const StepIO<float, float> &io,
-                                             float *abuf, bool stage) {
+                                             double *pbuf, uint64_t *kb) {
     constexpr int CH = NvRoll<LT>::CH, NP = NvRoll<LT>::NP;
     const int64_t S = P.cm.Npad;
     {   // both waves draw PTRS candidates: each writes the whole (identical) table
@@ -1006,7 +990,6 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
         const int nd = len - (rs ? 1 : 0);                   // the reset step draws none
         int64_t *dcol = dbuf + cb * CH * WAVE;
         const uint64_t ph0 = P.cm.ph_step + (uint64_t)k0;    // launch step of the chunk's first step
-        if (stage && role == 1) nv_load_actions(io, k0, len, P.cm.N, el, abuf + cb * CH * WAVE);
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
         for (int j = role; j < nd; j += 2) dcol[j * WAVE + lane] = 20;
 #else
@@ -1062,7 +1045,6 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
             }
         }
 #endif
-        if (stage && role == 1) nv_wait_actions();
         double *pb = pbuf + cb * NP * WAVE + lane;
         if (rs && role == 0) {                                // reset() at launch step k0 + len - 1
             st.g.set_step(ph0 + (uint64_t)(len - 1));
@@ -1083,6 +1065,7 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
         k0 += len;
         cb ^= 1;
     }
+    nv_wg_sync();   // barrier nch: the obs wave's last chunk
     if (valid && reset_any && role == 0) {
 #pragma unroll
         for (int j = 0; j < 5; j++) P.par[j * S + e] = st.par[j];
@@ -1093,9 +1076,27 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
 // step's order (OrderUpTo / ClassicNV / (s, S) / Constant, as nv_run_kernel)
 // instead of loading it; every output optional, the per-env sums in registers.
 // RG = PhiloxGen (the fast stream, newsvendor_ph.hip): the stream waves run
-// nv_stream_ph instead (above); the dynamics wave is the same.
+// nv_stream_ph instead (above); the dynamics and obs waves are the same.
+//
+// Round 4: four waves per 64 envs.  A wave issues at most about one
+// instruction every 9 cycles, and a SIMD about one every 3 with four or more
+// waves (tools/valu_rates, profiles/r04/launch/valu_rates.txt), so a step whose
+// instructions all sit on one wave runs at that wave's issue rate while the
+// SIMD idles.  The step therefore splits over two waves:
+//   wave 2 (dynamics) the step's state and reward (:125-170) with the pipeline
+//                     in registers; it hands the new order q and the reward to
+//                     wave 3 in LDS (hq, hr; a reset's params in hp) and writes
+//                     no global memory in its loop (the ring slots once, at the
+//                     end), so the action it loads a step ahead waits for
+//                     nothing but itself
+//   wave 3 (obs)      keeps its own copy of the pipeline from the handed-over
+//                     orders, writes the tile row, stores the tile, reward and
+//                     flags, one chunk behind the dynamics wave
+// Chunk c: the stream waves fill it before barrier c, the dynamics wave
+// consumes it between barriers c and c + 1, the obs wave between c + 1 and
+// c + 2 (every wave passes nch + 1 barriers).
 template <int LT, bool POL, class RG = Pcg>
-__global__ void __launch_bounds__(3 * WAVE)
+__global__ void __launch_bounds__(4 * WAVE)
 nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     using R = NvRoll<LT>;
     constexpr int O = R::O, CH = R::CH, NP = R::NP;
@@ -1108,8 +1109,9 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     double *ubuf = pbuf + 2 * NP * WAVE;                                   // [WAVE] mult wave's uniforms
     uint64_t *jt = reinterpret_cast<uint64_t *>(ubuf + WAVE);              // [4][JUMP_MAX + 1] jump table
     uint64_t *kb = jt + 4 * (JUMP_MAX + 1);                                // [2][2][WAVE] fast stream: keys, rates
-    float *abuf = reinterpret_cast<float *>(kb + 2 * 2 * WAVE);            // [2][CH][WAVE] staged actions
-    constexpr bool stage = !POL;                                          // actions through LDS
+    double *hr = reinterpret_cast<double *>(kb + 2 * 2 * WAVE);            // [2][CH][WAVE] rewards
+    float *hq = reinterpret_cast<float *>(hr + 2 * CH * WAVE);             // [2][CH][WAVE] new orders
+    float *hp = hq + 2 * CH * WAVE;                                        // [2][5][WAVE] a reset's params
     const int lane = threadIdx.x & (WAVE - 1);
     const int role = threadIdx.x / WAVE;
     const int64_t N = P.cm.N;
@@ -1123,7 +1125,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     const bool nxt = P.cm.autoreset == AR_NEXT_STEP;
     if constexpr (RG::kCounter) {
         if (role < 2) {   // ---- the fast stream's two stream waves
-            nv_stream_ph<LT>(P, role, lane, e, el, valid, t_start, K, nxt, lg_l, dbuf, pbuf, kb, io, abuf, stage);
+            nv_stream_ph<LT>(P, role, lane, e, el, valid, t_start, K, nxt, lg_l, dbuf, pbuf, kb);
             return;
         }
     }
@@ -1155,7 +1157,6 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             nv_chunk(t, K - k0, P.step_limit, nxt, CH, len, rs);
             const int nd = mine ? len - (rs ? 1 : 0) : 0;    // draws of this lane (the reset step draws none)
             int64_t *db = dbuf + cb * CH * WAVE + lane;
-            if (stage && multw) nv_load_actions(io, k0, len, N, el, abuf + cb * CH * WAVE);
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
             for (int j = 0; j < nd; j++) db[j * WAVE] = 20;
 #else
@@ -1209,7 +1210,6 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 }
             }
 #endif
-            if (stage && multw) nv_wait_actions();
             double *pb = pbuf + cb * NP * WAVE + lane;
 #ifdef INVSIM_TIMING
             if (ci < 4) TPROBE_W(2 + ci);
@@ -1238,6 +1238,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             k0 += len;
             cb ^= 1;
         }
+        nv_wg_sync();   // barrier nch: the obs wave's last chunk
         if (valid) {
             if (mine) P.cm.rng.store_state(e, st.g);
             if (reset_any && !multw) {
@@ -1249,8 +1250,80 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
         TPROBE_W(6);
         return;
     }
+    if (role == 3) {   // ---- obs wave
+        float *trow = tile + lane * O;
+        int sc = t_start;
+        float pf[5], pv[LT];
+#pragma unroll
+        for (int j = 0; j < 5; j++) pf[j] = (float)P.par[j * S + el];
+        {
+            const int base = (int)((uint32_t)(sc + 1) % (uint32_t)LT);
+#pragma unroll
+            for (int p = 0; p < LT; p++) {
+                int sl = base + p;
+                sl = sl >= LT ? sl - LT : sl;
+                pv[p] = P.pipe[(int64_t)sl * S + el];
+                if (!(p >= LT - sc)) pv[p] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 5; j++) trow[j] = pf[j];   // the params part changes only at a reset
+        int kk = 0, cb = 0;
+        nv_wg_sync();   // barrier 0
+        nv_wg_sync();   // barrier 1: chunk 0 handed over
+        TPROBE_W(1);
+        int ci = 0;
+        (void)ci;
+        for (int k = 0; k < K; k++) {
+            const int64_t oi = (int64_t)k * N + e;
+            const bool rs = nxt && sc >= P.step_limit;
+            double r = 0.0;
+            bool tr = false;
+            if (rs) {                                              // NEXT_STEP autoreset: the new params, empty pipeline
+#pragma unroll
+                for (int j = 0; j < 5; j++) {
+                    pf[j] = hp[(cb * 5 + j) * WAVE + lane];
+                    trow[j] = pf[j];
+                }
+#pragma unroll
+                for (int p = 0; p < LT; p++) pv[p] = 0.f;
+                sc = 0;
+            } else {
+                const float q = hq[(cb * CH + kk) * WAVE + lane];
+                r = hr[(cb * CH + kk) * WAVE + lane];
+#pragma unroll
+                for (int p = 0; p + 1 < LT; p++) pv[p] = pv[p + 1];
+                pv[LT - 1] = q;
+                tr = sc + 1 >= P.step_limit;                       // :190
+                sc += 1;
+            }
+#pragma unroll
+            for (int p = 0; p < LT; p++) trow[5 + p] = pv[p];      // obs after :183
+            if (valid && (!POL || io.rew)) {
+                out_store(io.rew + oi, r);
+                out_store(io.term + oi, (uint8_t)0);
+                out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
+            }
+            wave_lds_sync();
+#ifndef INVSIM_ABL_ROLL_NO_STORE
+            if (!POL || io.obs) store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+#endif
+            wave_lds_sync();
+            if (++kk == CH || rs || k == K - 1) {      // chunk consumed
+#ifdef INVSIM_TIMING
+                if (ci < 4) TPROBE_W(2 + ci);
+                ci++;
+#endif
+                if (k + 1 < K) nv_wg_sync();             // barrier of the next chunk's handoff
+                kk = 0;
+                cb ^= 1;
+            }
+        }
+        TWAIT();
+        TPROBE_W(6);
+        return;
+    }
     // ---- dynamics wave
-    float *trow = tile + lane * O;
     NvState<LT> st;
     int sc = t_start;
 #pragma unroll
@@ -1265,13 +1338,14 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             if (!(p >= LT - sc)) st.pv[p] = 0.f;
         }
     }
-    float nact = 0.f;
+    float nact = POL ? 0.f : io.act[el];
     constexpr int MD = 2;                       // metrics: reward sum, steps
     double met[MD];
 #pragma unroll
     for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
     double lvl = 0.0;     // CLASSIC_NV / SS: the episode's ppf level, once computed
     bool have = false;
+    int64_t dlast = -1;   // the last step's demand (the info record), -1: a reset step
     int kk = 0, cb = 0;
     int ci = 0;
     (void)ci;
@@ -1280,23 +1354,19 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     for (int k = 0; k < K; k++) {
         const int64_t oi = (int64_t)k * N + e;
         float act = nact;
-        if (stage) act = abuf[(cb * CH + kk) * WAVE + lane];       // staged by the mult stream wave
+        if (!POL && k + 1 < K) nact = io.act[(int64_t)(k + 1) * N + el];   // the next step's action
         const bool rs = nxt && sc >= P.step_limit;
         if (rs) {                                                  // NEXT_STEP autoreset
 #pragma unroll
-            for (int j = 0; j < 5; j++) st.par[j] = pbuf[(cb * NP + j) * WAVE + lane];
+            for (int j = 0; j < 5; j++) {
+                st.par[j] = pbuf[(cb * NP + j) * WAVE + lane];
+                hp[(cb * 5 + j) * WAVE + lane] = (float)st.par[j];   // -> obs wave
+            }
 #pragma unroll
             for (int p = 0; p < LT; p++) st.pv[p] = 0.f;
-            obs_params(st.par, trow);
-#pragma unroll
-            for (int j = 0; j < LT; j++) trow[5 + j] = 0.f;
-            if (valid && (!POL || io.rew)) {
-                out_store(io.rew + oi, 0.0);
-                out_store(io.term + oi, (uint8_t)0);
-                out_store(io.trunc + oi, (uint8_t)0);
-            }
             have = false;
             sc = 0;
+            dlast = -1;
         } else {
             if (POL) {
                 if (pol.kind == POL_ORDER_UP_TO) act = nv_order_up_to<LT>(P, pol, e, sc, st);
@@ -1307,38 +1377,40 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             }
             const int64_t d = dbuf[(cb * CH + kk) * WAVE + lane];
             double r;
-            const bool tr = nv_step_regs<LT>(P, e, valid, sc, st, act, trow, lg_l, nullptr, r,
-                                             (valid && k == K - 1) ? P.cm.info_demand : nullptr, d,
-                                             (valid && k == K - 1) ? (double *)P.cm.info_rec : nullptr);
+            nv_step_regs<LT>(P, e, valid, sc, st, act, nullptr, lg_l, nullptr, r, nullptr, d,
+                             (valid && k == K - 1) ? (double *)P.cm.info_rec : nullptr, false);
             if (POL) {
                 met[0] += r;                    // episode_reward += reward (benchmark_newsvendor.py:241)
                 met[1] += 1.0;
             }
-            if (valid && (!POL || io.rew)) {
-                out_store(io.rew + oi, r);
-                out_store(io.term + oi, (uint8_t)0);
-                out_store(io.trunc + oi, (uint8_t)(tr ? 1 : 0));
-            }
+            hq[(cb * CH + kk) * WAVE + lane] = st.pv[LT - 1];     // the new order -> obs wave
+            hr[(cb * CH + kk) * WAVE + lane] = r;
+            dlast = d;
             sc += 1;
         }
-        wave_lds_sync();
-#ifndef INVSIM_ABL_ROLL_NO_STORE
-        if (!POL || io.obs) store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
-#endif
-        wave_lds_sync();
         if (++kk == CH || rs || k == K - 1) {      // chunk consumed
 #ifdef INVSIM_TIMING
             if (ci < 4) TPROBE_W(2 + ci);
             ci++;
 #endif
-            if (k + 1 < K) nv_wg_sync();             // barrier of the next chunk
+            nv_wg_sync();                            // barrier of the next chunk (after the last: the obs wave's)
             kk = 0;
             cb ^= 1;
         }
     }
-    if (POL && valid && pol.metrics) {
+    if (valid) {
+        const int base = (int)((uint32_t)(sc + 1) % (uint32_t)LT);   // the ring slots of the final pipeline
 #pragma unroll
-        for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
+        for (int p = 0; p < LT; p++) {
+            int sl = base + p;
+            sl = sl >= LT ? sl - LT : sl;
+            P.pipe[(int64_t)sl * S + e] = st.pv[p];
+        }
+        if (P.cm.info_demand && dlast >= 0) P.cm.info_demand[e] = dlast;
+        if (POL && pol.metrics) {
+#pragma unroll
+            for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
+        }
     }
     TWAIT();
     TPROBE_W(6);
@@ -1467,7 +1539,7 @@ hipError_t nv_launch_rg(const NvParams &p, int t_u, const PolicyIO *pol, const S
     }
     if ((!pol || nv_pol_roll_enabled()) && io.K > 1 && t_u >= 0 && p.L > 0 &&
         p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
-        const dim3 gr(grid_for(p.cm.N, WAVE)), br(3 * WAVE);
+        const dim3 gr(grid_for(p.cm.N, WAVE)), br(4 * WAVE);
         bool done = true;
 #define R_(X)                                                                                              \
     do {                                                                                                   \

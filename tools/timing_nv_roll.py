@@ -1,14 +1,15 @@
-"""Per-wave timeline of the Newsvendor K=30 rollout (nv_roll_kernel, 3 waves
+"""Per-wave timeline of the Newsvendor K=30 rollout (nv_roll_kernel, 4 waves
 per 64-env workgroup: PTRS stream wave, multiplication stream wave, dynamics
-wave).  Profiling only; needs the TIMING build (csrc `make timing`):
+wave, obs wave).  Profiling only; needs the TIMING build (csrc `make timing`):
 
   INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so python tools/timing_nv_roll.py
 
-Probes (s_memrealtime, 100 MHz, lane 0 of every wave, row = workgroup * 3 +
+Probes (s_memrealtime, 100 MHz, lane 0 of every wave, row = workgroup * 4 +
 wave): 0 entry, 1 ready (stream: state + tables loaded; dynamics: barrier 0
-passed), 2-5 chunk c = 0..3 (stream: its draws done, before the chunk's
-barrier; dynamics: the chunk consumed, before the next barrier), 6 exit
-(stores drained), 7 hardware ids (XCC, SE/CU/SIMD/wave slot).
+passed; obs: barrier 1 passed), 2-5 chunk c = 0..3 (stream: its draws done,
+before the chunk's barrier; dynamics / obs: the chunk consumed, before the
+next barrier), 6 exit (stores drained), 7 hardware ids (XCC, SE/CU/SIMD/wave
+slot).
 """
 import ctypes as C
 import os
@@ -35,14 +36,15 @@ def main():
     buf = np.zeros((4096, 8), dtype=np.uint64)
     rc = _capi.lib().invsim_debug_timing_nv(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
     assert rc == 0, rc
-    W = 3 * (n // 64)
+    R = 4
+    W = R * (n // 64)
     b = buf[:W].astype(np.int64)
     t0 = b[:, 0].min()
     pct = [0, 10, 50, 90, 100]
     fmt = lambda x: " ".join(f"{v * 10.0:8.0f}" for v in np.percentile(x, pct))  # noqa: E731
     print("ns percentiles        p0       p10      p50      p90      max")
-    for role, name in ((0, "PTRS stream"), (1, "mult stream"), (2, "dynamics")):
-        sel = b[role::3]
+    for role, name in ((0, "PTRS stream"), (1, "mult stream"), (2, "dynamics"), (3, "obs")):
+        sel = b[role::R]
         print(f"-- {name}: {len(sel)} waves")
         print("  entry          " + fmt(sel[:, 0] - t0))
         print("  ready          " + fmt(sel[:, 1] - t0))
@@ -52,7 +54,7 @@ def main():
             prev = sel[:, 2 + c]
         print("  exit           " + fmt(sel[:, 6] - t0))
     # per chunk: how long the dynamics wave waited at the barrier for its stream waves
-    d, p, m = b[2::3], b[0::3], b[1::3]
+    d, p, m = b[2::R], b[0::R], b[1::R]
     for c in range(3):
         ready = np.maximum(p[:, 3 + c], m[:, 3 + c])          # chunk c+1 drawn by both stream waves
         wait = np.maximum(0, ready - d[:, 2 + c])
@@ -68,7 +70,9 @@ def main():
     key = (((xcc * 8 + se) * 2 + sh) * 16 + cu) * 4 + simd
     _, cnt = np.unique(key, return_counts=True)
     print("waves per SIMD: " + " ".join(f"{k}:{v}" for k, v in zip(*np.unique(cnt, return_counts=True))))
-    ptrs_key = key[0::3]
+    ptrs_key = key[0::R]
+    same = np.mean([len(set(key[w * R:(w + 1) * R])) == 1 for w in range(W // R)])
+    print("workgroups with all %d waves on one SIMD: %.1f %%" % (R, 100.0 * same))
     share = np.array([np.sum(ptrs_key == k) for k in ptrs_key])
     print("PTRS waves sharing their SIMD with another PTRS wave: %.1f %%" % (100.0 * np.mean(share > 1)))
     print(f"kernel span {(b[:, 6].max() - t0) * 10.0:.0f} ns")
