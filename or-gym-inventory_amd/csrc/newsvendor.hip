@@ -1399,12 +1399,15 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
         }
     }
     if (valid) {
-        const int base = (int)((uint32_t)(sc + 1) % (uint32_t)LT);   // the ring slots of the final pipeline
+        // the ring slots of the final pipeline: the positions this episode has
+        // ordered (p >= LT - sc; the others are masked at load and keep their
+        // bytes, as the per-step slot writes of the other kernels leave them)
+        const int base = (int)((uint32_t)(sc + 1) % (uint32_t)LT);
 #pragma unroll
         for (int p = 0; p < LT; p++) {
             int sl = base + p;
             sl = sl >= LT ? sl - LT : sl;
-            P.pipe[(int64_t)sl * S + e] = st.pv[p];
+            if (p >= LT - sc) P.pipe[(int64_t)sl * S + e] = st.pv[p];
         }
         if (P.cm.info_demand && dlast >= 0) P.cm.info_demand[e] = dlast;
         if (POL && pol.metrics) {
