@@ -1357,6 +1357,15 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
         if (!POL && k + 1 < K) nact = io.act[(int64_t)(k + 1) * N + el];   // the next step's action
         const bool rs = nxt && sc >= P.step_limit;
         if (rs) {                                                  // NEXT_STEP autoreset
+            if (valid) {   // the ending episode's ring slots, as its per-step slot writes leave them
+                const int base = (int)((uint32_t)(sc + 1) % (uint32_t)LT);
+#pragma unroll
+                for (int p = 0; p < LT; p++) {
+                    int sl = base + p;
+                    sl = sl >= LT ? sl - LT : sl;
+                    if (p >= LT - sc) P.pipe[(int64_t)sl * S + e] = st.pv[p];
+                }
+            }
 #pragma unroll
             for (int j = 0; j < 5; j++) {
                 st.par[j] = pbuf[(cb * NP + j) * WAVE + lane];
@@ -1400,8 +1409,8 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     }
     if (valid) {
         // the ring slots of the final pipeline: the positions this episode has
-        // ordered (p >= LT - sc; the others are masked at load and keep their
-        // bytes, as the per-step slot writes of the other kernels leave them)
+        // ordered (p >= LT - sc; the others are masked at load and keep the
+        // bytes the per-step slot writes of the other kernels leave there)
         const int base = (int)((uint32_t)(sc + 1) % (uint32_t)LT);
 #pragma unroll
         for (int p = 0; p < LT; p++) {
