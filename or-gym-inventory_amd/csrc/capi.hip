@@ -671,8 +671,6 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
         p.rl_p = tab<double>(h, t_rp);
         p.rl_b = tab<double>(h, t_rb);
         p.rl_pc = tab<PtrsConst>(h, t_pc);
-        p.rhs_nk_max = 0;
-        for (int r = 0; r < RL; r++) p.rhs_nk_max = std::max(p.rhs_nk_max, pcs[r].nk);
         p.rl_dist = any_npd ? tab<int32_t>(h, t_rd) : nullptr;
         p.rl_nd = tab<NpDist>(h, t_rnd);
         if (o_U32 >= 0) h->cm.u32buf = at<uint64_t>(h, o_U32);

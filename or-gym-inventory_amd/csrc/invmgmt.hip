@@ -575,9 +575,11 @@ im_reset_kernel(ImParams P, const uint8_t *__restrict__ mask, int64_t *__restric
 // __syncthreads() would also drain each wave's outstanding global loads and
 // stores, s_waitcnt vmcnt(0), before the s_barrier)
 __device__ __forceinline__ void wg_lds_sync() {
+    TBAR_T0();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    TBAR_ADD();
 }
 
 // Single lock-step step (invsim_step, K = 1, t_u < periods, no SAME_STEP reset
@@ -1382,6 +1384,8 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
     const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
     const int K = io.K;
     const int nch = (K + CH - 1) / CH;
+    TPROBE_W(0);
+    TPROBE_W_ID();
     if (role == 0) {   // ---- demand wave
         TableStage ts;
         ts.dst = rhs_l;
@@ -1404,6 +1408,8 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
             im_stream_loop<CH, G::RD>(P, g, rhs_l, dbuf, lane, K, nch + 1, t_start, stage);
         }
         if (valid) P.cm.rng.store_state(e, g);
+        TWAIT();
+        TPROBE_W(6);
         return;
     }
     if (role == 2) {   // ---- obs wave
@@ -1490,6 +1496,8 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
                 wave_lds_sync();
             }
         }
+        TWAIT();
+        TPROBE_W(6);
         return;
     }
     // ---- dynamics wave
@@ -1697,6 +1705,8 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
             for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
         }
     }
+    TWAIT();
+    TPROBE_W(6);
 }
 
 // cm.rng <- the committed slot of the lookahead cache (see im_split_kernel)
@@ -1997,5 +2007,8 @@ INVSIM_PTRS_STATS_TU(im)
 #if defined(INVSIM_TIMING) && !defined(INVSIM_IM_FAST_TU)
 extern "C" int invsim_debug_timing(void *dst, int64_t bytes) {
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_tbuf), (size_t)bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int invsim_debug_timing_bar(void *dst, int64_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_tbar), (size_t)bytes, 0, hipMemcpyDeviceToHost);
 }
 #endif

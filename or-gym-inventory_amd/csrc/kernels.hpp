@@ -47,13 +47,27 @@ constexpr int TB_WAVES = 4096, TB_PROBES = 8;   // probe 7: hardware ids
 #define TPROBE_W_ID()                                                                          \
     do {                                                                                       \
         const unsigned tw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;                \
-        if ((threadIdx.x & 63) == 0 && tw_ < (unsigned)TB_WAVES)                               \
+        if ((threadIdx.x & 63) == 0 && tw_ < (unsigned)TB_WAVES) {                             \
             g_tbuf[tw_ * TB_PROBES + 7] =                                                      \
                 ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |                 \
                 (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                           \
+            g_tbar[tw_] = 0;                                                                   \
+        }                                                                                      \
+    } while (0)
+// accumulated barrier wait of each wave (the rollout kernels' workgroup
+// syncs): g_tbar[wave row] (100 MHz ticks), zeroed by TPROBE_W_ID at entry
+static __device__ uint64_t g_tbar[TB_WAVES];
+#define TBAR_T0() const uint64_t tb0_ = __builtin_amdgcn_s_memrealtime()
+#define TBAR_ADD()                                                                             \
+    do {                                                                                       \
+        const unsigned tw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;                \
+        if ((threadIdx.x & 63) == 0 && tw_ < (unsigned)TB_WAVES)                               \
+            g_tbar[tw_] += __builtin_amdgcn_s_memrealtime() - tb0_;                            \
     } while (0)
 #define TWAIT() __builtin_amdgcn_s_waitcnt(0)
 #else
+#define TBAR_T0() do {} while (0)
+#define TBAR_ADD() do {} while (0)
 #define TPROBE_W(i) do {} while (0)
 #define TPROBE_W_ID() do {} while (0)
 #define TPROBE_AT(i, tid) do {} while (0)
@@ -144,7 +158,6 @@ struct NetParams {
     const double *user_D;        // [RL][T]
     const int32_t *succ_ptr, *succ_kind, *succ_idx, *pred_ptr, *pred_idx;
     const double *alpha_pow;     // [T]
-    int32_t rhs_nk_max;          // host: the longest PTRS RHS table of a market (0: none)
     // state
     double *X;                   // [J][Npad]
     double *U;                   // [RL][Npad]
@@ -316,9 +329,11 @@ __device__ __forceinline__ void store_tile(const T *__restrict__ tile, T *__rest
 // __syncthreads() would also drain each wave's outstanding global loads and
 // stores, s_waitcnt vmcnt(0), before the s_barrier)
 __device__ __forceinline__ void roll_wg_sync() {
+    TBAR_T0();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    TBAR_ADD();
 }
 
 // One numpy random_poisson attempt for a fixed-rate stream: a PTRS candidate

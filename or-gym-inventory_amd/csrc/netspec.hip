@@ -71,10 +71,10 @@ __device__ __forceinline__ void spec_demand(RG &g, const PtrsConst (&pc)[G::RL],
 
 // The demand wave of the rollout kernels (stream_flat_loop): the market demands
 // of each launch step, retail-link order, into the ring dbuf [RD * CH][RL][WAVE]
-template <class G, int CH, int RD, class RG, class Stage = NoStage>
+template <class G, int CH, int RD, class RG>
 __device__ __forceinline__ void net_demand_loop(RG &g, const PtrsConst (&pc)[G::RL], const double *rhs_l,
                                                 double *dbuf, int lane, int K, int nb, int t_start, int T,
-                                                uint64_t ph_step, int rs = RHS_LDS_MAX, Stage stage = Stage()) {
+                                                uint64_t ph_step) {
     constexpr int RL = G::RL;
     StreamPos<RG> pos(ph_step);
     stream_flat_loop<CH, RD, RL>(
@@ -87,7 +87,7 @@ __device__ __forceinline__ void net_demand_loop(RG &g, const PtrsConst (&pc)[G::
             for (int q = 1; q < RL; q++)
                 if (r == q) {
                     c = pc[q];
-                    rt = rhs_l + q * rs;
+                    rt = rhs_l + q * RHS_LDS_MAX;
                 }
 #ifdef INVSIM_ABL_ROLL_NO_DRAW
             kd = 20;
@@ -98,40 +98,8 @@ __device__ __forceinline__ void net_demand_loop(RG &g, const PtrsConst (&pc)[G::
         },
         [&](int slot, int r, int64_t kd) {   // max(0, int(round(poisson(lam)))) (:536-541)
             dbuf[(slot * RL + r) * WAVE + lane] = (double)(kd > 0 ? kd : 0);
-        },
-        stage);
+        });
 }
-
-// The open-loop 3-role rollout's actions of chunk b (E f32 per env and step),
-// staged into the LDS ring act_l [2][CH][E][WAVE] by the demand wave with
-// LDS-DMA loads (global_load_lds_dword: row q of step kk lands at + q * WAVE,
-// lane l at + 4 l); chunk b is read by the dynamics wave between barriers b and
-// b + 1, and its buffer (b & 1) was last read before barrier b - 1.
-template <int CH, int E>
-struct NetActStage {
-    const float *act;
-    float *act_l;
-    int64_t N, el;
-    int K, nch;
-    __device__ __forceinline__ void operator()(int b) const {
-        if (b >= nch) return;
-#pragma unroll
-        for (int kk = 0; kk < CH; kk++) {
-            const int k = b * CH + kk;
-            if (k < K) {
-                const float *src = act + ((int64_t)k * N + el) * E;
-#pragma unroll
-                for (int q = 0; q < E; q++)
-                    __builtin_amdgcn_global_load_lds(
-                        (const void *)(src + q),
-                        (__attribute__((address_space(3))) void *)(act_l + (((b & 1) * CH + kk) * E + q) * WAVE), 4,
-                        0, 0);
-            }
-        }
-    }
-    __device__ __forceinline__ void wait() const { __builtin_amdgcn_s_waitcnt(0); }
-};
-constexpr int NET_AP_LDS = 48;   // alpha**t LDS table of the 3-role rollout (T <= this)
 
 // One step (:436-635) at period t < T given the step's market demands Dd; obs
 // row into orow (LDS).  Returns the reward; Rn receives R[t] (the fulfilled
@@ -1124,28 +1092,20 @@ struct NetLpos {
 #define NET_ROLL3_CH 2   // chunk of the 3-role rollout (LDS: two 192-thread workgroups per CU)
 #endif
 #ifndef NET_ROLL3_RD
-#define NET_ROLL3_RD 4   // demand ring depth in chunks (>= 2): how far the demand wave may run ahead
-#endif                   // ((2, 8) and (2, 4) measured equal in round 3; 4 leaves LDS for the staged actions)
+#define NET_ROLL3_RD 8   // demand ring depth in chunks (>= 2): how far the demand wave may run ahead
+#endif
 
-// LDS: tile | demand ring | fulfilled-order ring | rec | staged actions |
-// alpha**t | PTRS RHS tables, the last sized at launch (rs entries per market:
-// the longest table, not RHS_LDS_MAX), so that two workgroups share a CU
 template <class G, int CH_>
 struct NetRoll3 {
     static constexpr int CH = CH_;
     static constexpr int NR = G::RL + G::J + NetLpos<G>::count();   // rec columns per step
     static constexpr size_t tile_bytes() { return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float); }
+    static constexpr size_t rhs_bytes() { return (size_t)G::RL * RHS_LDS_MAX * sizeof(double); }
     static constexpr int RD = NET_ROLL3_RD;
     static constexpr size_t dbuf_bytes() { return (size_t)RD * CH * G::RL * WAVE * sizeof(double); }
     static constexpr size_t ring_bytes() { return (size_t)(G::sumL > 0 ? G::sumL : 1) * WAVE * sizeof(double); }
     static constexpr size_t rec_bytes() { return 2 * (size_t)CH * NR * WAVE * sizeof(float); }
-    static constexpr size_t act_bytes() { return 2 * (size_t)CH * G::E * WAVE * sizeof(float); }
-    static constexpr size_t ap_bytes() { return (size_t)NET_AP_LDS * sizeof(double); }
-    static constexpr size_t fixed() {
-        return tile_bytes() + dbuf_bytes() + ring_bytes() + rec_bytes() + act_bytes() + ap_bytes();
-    }
-    static int rs(const NetParams &p) { return p.rhs_nk_max > 0 ? p.rhs_nk_max : 1; }
-    static size_t lds(const NetParams &p) { return fixed() + (size_t)G::RL * rs(p) * sizeof(double); }
+    static constexpr size_t lds() { return tile_bytes() + rhs_bytes() + dbuf_bytes() + ring_bytes() + rec_bytes(); }
 };
 
 // POL (invsim_rollout_policy with CONSTANT, ConstantOrderAgent,
@@ -1163,14 +1123,11 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO po
     extern __shared__ __attribute__((aligned(16))) float n3_lds[];
     char *lb = reinterpret_cast<char *>(n3_lds);
     float *tile = n3_lds;
-    double *dbuf = reinterpret_cast<double *>(lb + R3::tile_bytes());                      // [RD * CH][RL][WAVE]
-    double *ring = reinterpret_cast<double *>(lb + R3::tile_bytes() + R3::dbuf_bytes());
-    float *rec = reinterpret_cast<float *>(lb + R3::tile_bytes() + R3::dbuf_bytes() +
+    double *rhs_l = reinterpret_cast<double *>(lb + R3::tile_bytes());
+    double *dbuf = reinterpret_cast<double *>(lb + R3::tile_bytes() + R3::rhs_bytes());     // [RD * CH][RL][WAVE]
+    double *ring = reinterpret_cast<double *>(lb + R3::tile_bytes() + R3::rhs_bytes() + R3::dbuf_bytes());
+    float *rec = reinterpret_cast<float *>(lb + R3::tile_bytes() + R3::rhs_bytes() + R3::dbuf_bytes() +
                                            R3::ring_bytes());                              // [2][CH][NR][WAVE]
-    float *act_l = rec + 2 * CH * NR * WAVE;                                               // [2][CH][E][WAVE]
-    double *ap_l = reinterpret_cast<double *>(act_l + 2 * CH * G::E * WAVE);               // alpha**t, t < T
-    double *rhs_l = ap_l + NET_AP_LDS;                                                     // [RL][rs]
-    const int rs = P.rhs_nk_max > 0 ? P.rhs_nk_max : 1;
     const int lane = threadIdx.x & (WAVE - 1);
     const int role = threadIdx.x / WAVE;
     const int64_t N = P.cm.N;
@@ -1200,19 +1157,11 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO po
 #pragma unroll
         for (int r = 0; r < RL; r++)
 #pragma unroll
-            for (int u = 0; u < NT; u++)
-                if (lane + u * WAVE < rs) rhs_l[r * rs + lane + u * WAVE] = tv[r][u];
-        for (int q = lane; q < P.T; q += WAVE) ap_l[q] = P.alpha_pow[q];   // read after barrier 0
+            for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
         wave_lds_sync();
         // flat draw loop (stream_flat_loop): up to RD chunks ahead of the dynamics;
         // barriers 0 .. nch - 1 (demand chunk c ready), nch (the obs wave's last chunk)
-        if (POL) {
-            net_demand_loop<G, CH, RD>(g, pc, rhs_l, dbuf, lane, K, nch + 1, t_start, P.T, P.cm.ph_step, rs);
-        } else {
-            const NetActStage<CH, G::E> stage{io.act, act_l, N, el, K, nch};
-            net_demand_loop<G, CH, RD>(g, pc, rhs_l, dbuf, lane, K, nch + 1, t_start, P.T, P.cm.ph_step, rs,
-                                       stage);
-        }
+        net_demand_loop<G, CH, RD>(g, pc, rhs_l, dbuf, lane, K, nch + 1, t_start, P.T, P.cm.ph_step);
         if (valid) P.cm.rng.store_state(e, g);
         return;
     }
@@ -1296,10 +1245,14 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO po
 #pragma unroll
         for (int q = 0; q < G::sumL; q++) rg[q * WAVE] = rv[q];
     }
+    float nact[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; k++) nact[k] = POL ? pol.cf[k] : io.act[el * G::E + k];
     constexpr int MD = 5 + G::J;             // metrics: reward, steps, demand, sales, stockout, X per node
     double met[MD];
 #pragma unroll
     for (int q = 0; q < MD; q++) met[q] = (POL && pol.metrics) ? pol.metrics[el * MD + q] : 0.0;
+    double napow = P.alpha_pow[t < P.T ? t : 0];
     double dlast[RL];
 #pragma unroll
     for (int r = 0; r < RL; r++) dlast[r] = 0.0;
@@ -1312,11 +1265,18 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO po
         for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
             const int k = c * CH + kk;
             const int64_t oi = (int64_t)k * N + e;
-            float act[G::E];                                    // staged by the demand wave (POL: the agent's)
+            float act[G::E];
 #pragma unroll
-            for (int q = 0; q < G::E; q++)
-                act[q] = POL ? pol.cf[q] : act_l[(((c & 1) * CH + kk) * G::E + q) * WAVE + lane];
-            const double apow = ap_l[t < P.T ? t : 0];
+            for (int q = 0; q < G::E; q++) act[q] = nact[q];
+            const double apow = napow;
+            {
+                const int tn = (t >= P.T) ? 0 : t + 1;          // the next launch step's period
+                napow = P.alpha_pow[tn < P.T ? tn : 0];
+            }
+            if (!POL && k + 1 < K) {                            // the next step's actions
+#pragma unroll
+                for (int q = 0; q < G::E; q++) nact[q] = io.act[((int64_t)(k + 1) * N + el) * G::E + q];
+            }
             if (t >= P.T) {                                     // NEXT_STEP autoreset (:301-332)
 #pragma unroll
                 for (int j = 0; j < G::J; j++) st.X[j] = G::I0[j];
@@ -1525,14 +1485,14 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
     } while (0)
     // ... and the in-kernel ConstantOrder agent on the 3-role kernel
     const bool pol_roll = pol && pol->kind == POL_CONSTANT && net_pol_roll_enabled();
-    if ((!pol || (pol_roll && p.T <= NET_AP_LDS)) && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
+    if ((!pol || pol_roll) && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
         (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
         const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE));
         using R3 = NetRoll3<G, NET_ROLL3_CH>;
 #define RK_(RG)                                                                                                       \
     do {                                                                                                              \
-        if (pol) hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, true, RG>), gr, dim3(3 * WAVE), R3::lds(p), s, p, t_u, io, pv); \
-        else if (net_roll3_use(p.cm.N) && p.T <= NET_AP_LDS) hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, false, RG>), gr, dim3(3 * WAVE), R3::lds(p), s, p, t_u, io, pv); \
+        if (pol) hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, true, RG>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv); \
+        else if (net_roll3_use(p.cm.N)) hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, false, RG>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv); \
         else hipLaunchKernelGGL((net_roll_kernel<G, RG>), gr, dim3(2 * WAVE), NetRoll<G>::lds(), s, p, t_u, io);    \
     } while (0)
         if (ph) RK_(PhiloxGen);

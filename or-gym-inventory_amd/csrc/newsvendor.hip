@@ -775,9 +775,11 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla, i
 }
 
 __device__ __forceinline__ void nv_wg_sync() {
+    TBAR_T0();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    TBAR_ADD();
 }
 
 // numpy's sampler branch of a rate: true = the multiplication method (0 < lam < 10;
@@ -1133,6 +1135,9 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     TPROBE_W_ID();
     if constexpr (!RG::kCounter) if (role < 2) {   // ---- stream waves
         const bool multw = role == 1;
+#ifdef NV_ROLL_PRIO
+        if (!multw) __builtin_amdgcn_s_setprio(NV_ROLL_PRIO);   // A/B: the PTRS wave first at issue
+#endif
         TableStage ts;
         if (!multw) {
             ts.dst = lg_l;
@@ -1624,5 +1629,8 @@ INVSIM_PTRS_STATS_TU(nv)
 #if defined(INVSIM_TIMING) && !defined(INVSIM_NV_FAST_TU)
 extern "C" int invsim_debug_timing_nv(void *dst, int64_t bytes) {
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_tbuf), (size_t)bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int invsim_debug_timing_bar_nv(void *dst, int64_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_tbar), (size_t)bytes, 0, hipMemcpyDeviceToHost);
 }
 #endif

@@ -1,0 +1,72 @@
+"""Per-wave lifetime and barrier wait of the InvMgmt 3-role rollout
+(im_roll3o: demand stream wave, dynamics wave, obs wave per 64 envs) on the
+LostSales K=30 workload.  Profiling only; needs the TIMING build (csrc
+`make timing`):
+
+  INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so python tools/timing_im_roll.py [n] [policy]
+
+Probes (s_memrealtime, 100 MHz, lane 0 of every wave, row = workgroup * 3 +
+wave): 0 entry, 6 exit (stores drained); g_tbar = the wave's accumulated wait
+in the workgroup syncs.  work = lifetime - wait is what the role itself
+issues; the role whose work is closest to the lifetime sets the pace.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "or-gym-inventory_amd"))
+
+
+def main():
+    import invsim
+    from invsim import _capi
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
+    policy = len(sys.argv) > 2 and sys.argv[2] == "policy"
+    K = 30
+    env = invsim.InvManagementLostSalesEnv(num_envs=n)
+    env.reset(seed=0)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    hi = torch.as_tensor(env.single_action_space.high, device=env.device)
+    M = hi.numel()
+    for _ in range(4):
+        if policy:
+            env.rollout_policy(invsim.policies.BaseStockAgent(), K)
+        else:
+            a = torch.floor(torch.rand((K, n, M), device=env.device, generator=g, dtype=torch.float64) * (hi + 1))
+            env.rollout(a.to(torch.int64))
+    torch.cuda.synchronize()
+    buf = np.zeros((4096, 8), dtype=np.uint64)
+    rc = _capi.lib().invsim_debug_timing(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
+    assert rc == 0, rc
+    bar = np.zeros(4096, dtype=np.uint64)
+    rc = _capi.lib().invsim_debug_timing_bar(bar.ctypes.data_as(C.c_void_p), C.c_int64(bar.nbytes))
+    assert rc == 0, rc
+    R = 3
+    W = R * ((n + 63) // 64)
+    assert W <= 4096, "TB_WAVES rows"
+    b = buf[:W].astype(np.int64)
+    bar = bar[:W].astype(np.int64)
+    t0 = b[:, 0].min()
+    pct = [0, 10, 50, 90, 100]
+    fmt = lambda x: " ".join(f"{v * 10.0:8.0f}" for v in np.percentile(x, pct))  # noqa: E731
+    print(f"InvMgmt LostSales n={n} K={K} {'policy' if policy else 'open-loop'} rollout, last launch")
+    print("ns percentiles          p0       p10      p50      p90      max")
+    for role, name in ((0, "demand stream"), (1, "dynamics"), (2, "obs")):
+        sel = b[role::R]
+        life = sel[:, 6] - sel[:, 0]
+        wt = bar[role::R]
+        print(f"-- {name}: {len(sel)} waves")
+        print("  entry        " + fmt(sel[:, 0] - t0))
+        print("  exit         " + fmt(sel[:, 6] - t0))
+        print("  lifetime     " + fmt(life))
+        print("  barrier wait " + fmt(wt))
+        print("  work         " + fmt(life - wt))
+    print(f"kernel span {(b[:, 6].max() - t0) * 10.0:.0f} ns")
+
+
+if __name__ == "__main__":
+    main()

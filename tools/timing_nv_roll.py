@@ -9,7 +9,8 @@ wave): 0 entry, 1 ready (stream: state + tables loaded; dynamics: barrier 0
 passed; obs: barrier 1 passed), 2-5 chunk c = 0..3 (stream: its draws done,
 before the chunk's barrier; dynamics / obs: the chunk consumed, before the
 next barrier), 6 exit (stores drained), 7 hardware ids (XCC, SE/CU/SIMD/wave
-slot).
+slot).  Also the accumulated barrier wait of every wave (g_tbar): the part of
+its lifetime spent in the workgroup syncs, the rest is its own work.
 """
 import ctypes as C
 import os
@@ -75,6 +76,15 @@ def main():
     print("workgroups with all %d waves on one SIMD: %.1f %%" % (R, 100.0 * same))
     share = np.array([np.sum(ptrs_key == k) for k in ptrs_key])
     print("PTRS waves sharing their SIMD with another PTRS wave: %.1f %%" % (100.0 * np.mean(share > 1)))
+    bar = np.zeros(4096, dtype=np.uint64)
+    rc = _capi.lib().invsim_debug_timing_bar_nv(bar.ctypes.data_as(C.c_void_p), C.c_int64(bar.nbytes))
+    assert rc == 0, rc
+    bar = bar[:W].astype(np.int64)
+    print("per role (last launch): lifetime = exit - entry, barrier wait, work = lifetime - wait")
+    for role, name in ((0, "PTRS stream"), (1, "mult stream"), (2, "dynamics"), (3, "obs")):
+        life = b[role::R, 6] - b[role::R, 0]
+        wt = bar[role::R]
+        print(f"  {name:12s} life {fmt(life)}\n  {'':12s} wait {fmt(wt)}\n  {'':12s} work {fmt(life - wt)}")
     print(f"kernel span {(b[:, 6].max() - t0) * 10.0:.0f} ns")
 
 
