@@ -293,6 +293,49 @@ __device__ __forceinline__ bool ptrs_log_accept(const PtrsConst &c, double V, do
     return (log(V) + c.log_invalpha - log(c.a / (us * us) + c.b)) <= r;
 }
 
+// One numpy PTRS candidate (the loop body of random_poisson_ptrs) from its two
+// uniforms, with the same decision as the branchy form above, laid out for a
+// lone wave: its three chains -- k (the f64 division and floor), the f32 log
+// test's inputs (us, V only) and the RHS table read (k only) -- are computed
+// for every lane without branches between them, so they interleave instead of
+// running one after the other; only a near-tie of the f32 test, x/us overflow
+// or k outside the table take the exact branch.  The f32 x = a/us^2 + b uses
+// v_rcp_f32 (1 ulp): relative error <= 10 * 2^-24, i.e. <= 2^-20 in log2,
+// within the input allowance of ptrs_log_accept's bound.
+// tab(k, ok): -lam + k log lam - loggam(k + 1) from an LDS table (ok = false:
+// k outside it, value unused); rhs(k): the same, exactly, on device.
+template <class Tab, class Rhs>
+__device__ __forceinline__ bool ptrs_decide(const PtrsConst &c, double U, double V, Tab tab, Rhs rhs, int64_t &k) {
+    constexpr double LN2 = 0.69314718055994530942;
+    const double us = 0.5 - fabs(U);
+    k = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+    const float us32 = (float)us;
+    const float x32 = (float)c.a * __builtin_amdgcn_rcpf(us32 * us32) + (float)c.b;
+    const float l2v = __builtin_amdgcn_logf((float)V);
+    const float l2x = __builtin_amdgcn_logf(x32);
+    bool ok;
+    const double r = tab(k, ok);
+    const bool qacc = (us >= 0.07) && (V <= c.vr);
+    const bool qrej = (k < 0) || ((us < 0.013) && (V > us));
+    const double lhs = ((double)l2v * LN2 + c.log_invalpha) - (double)l2x * LN2;
+    const double err = (fabs((double)l2v) + fabs((double)l2x)) * (LN2 * 0x1p-22) + LN2 * 0x1p-19 +
+                       (fabs(lhs) + fabs(r)) * 0x1p-40;
+    const bool fin = ok && (x32 < 1e30f);
+    const bool facc = fin && (lhs + err < r), frej = fin && (lhs - err > r);
+#ifdef INVSIM_PTRS_STATS
+    if (!qacc && !qrej && (facc || frej)) {   // f32-decided: count and check against the f64 test
+        const bool exact = (log(V) + c.log_invalpha - log(c.a / (us * us) + c.b)) <= r;
+        atomicAdd(&g_ptrs_stats[0], 1ull);
+        if (facc != exact) atomicAdd(&g_ptrs_stats[3], 1ull);
+    }
+#endif
+    // bitwise, not short-circuit: every lane computes every chain (no branch to sink them under)
+    const bool dec = qacc | qrej | facc | frej;
+    bool acc = qacc | (!qrej & facc);
+    if (!dec) acc = ptrs_log_accept(c, V, us, ok ? r : rhs(k));   // rare: the exact path
+    return acc;
+}
+
 // numpy random_poisson_ptrs (distributions.c), constants precomputed
 template <class G>
 __device__ inline int64_t np_poisson_ptrs(G &g, const PtrsConst &c, const double *rhs = nullptr) {

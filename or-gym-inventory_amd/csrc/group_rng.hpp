@@ -163,17 +163,41 @@ struct PtrsJumpLane {
     }
 };
 
+// Sources of the PTRS right-hand side  -lam + k log lam - loggam(k + 1):
+// fast(k, c, ok) reads an LDS table (ok = false: k outside it, value unused),
+// exact(k, c) computes it on device.
+struct RhsTab {   // host table of the whole right-hand side for k in [c.k0, c.k0 + c.nk) (fixed rates)
+    const double *t;
+    __device__ __forceinline__ double fast(int64_t k, const PtrsConst &c, bool &ok) const {
+        ok = k >= c.k0 && k < (int64_t)c.k0 + c.nk;
+        return t[ok ? (int)(k - c.k0) : 0];
+    }
+    __device__ __forceinline__ double exact(int64_t k, const PtrsConst &c) const { return ptrs_rhs(c, nullptr, k); }
+};
+// (LgTab, the Newsvendor table source, is in kernels.hpp beside RHS_LDS_MAX)
+
 // one PTRS candidate (numpy random_poisson_ptrs loop body) from two uniforms of
-// g; rhs(k, c) = -lam + k log lam - loggam(k + 1)
-template <class G, class Rhs>
-__device__ __forceinline__ bool ptrs_candidate(G &g, const PtrsConst &c, Rhs rhs, int64_t &k) {
+// g; src: RhsTab / LgTab.  INVSIM_PTRS_DECIDE=0 builds the branchy body (A/B).
+#ifndef INVSIM_PTRS_DECIDE
+#define INVSIM_PTRS_DECIDE 1
+#endif
+template <class G, class Src>
+__device__ __forceinline__ bool ptrs_candidate(G &g, const PtrsConst &c, const Src &src, int64_t &k) {
     const double U = g.next_double() - 0.5;
     const double V = g.next_double();
+#if INVSIM_PTRS_DECIDE
+    return ptrs_decide(
+        c, U, V, [&](int64_t kk, bool &ok) { return src.fast(kk, c, ok); },
+        [&](int64_t kk) { return src.exact(kk, c); }, k);
+#else
     const double us = 0.5 - fabs(U);
     k = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
     if ((us >= 0.07) && (V <= c.vr)) return true;
     if ((k < 0) || ((us < 0.013) && (V > us))) return false;
-    return ptrs_log_accept(c, V, us, rhs(k, c));
+    bool ok;
+    const double r = src.fast(k, c, ok);
+    return ptrs_log_accept(c, V, us, ok ? r : src.exact(k, c));
+#endif
 }
 
 // PTRS draw of the lane's env (c.lam >= 10 for every lane that calls it with
@@ -184,8 +208,8 @@ struct NoProbe {
     __device__ __forceinline__ void operator()(int) const {}
 };
 
-template <class Rhs, class ShflC, class Probe = NoProbe>
-__device__ __forceinline__ int64_t np_poisson_ptrs_compact(Pcg &g, const PtrsConst &c, Rhs rhs, bool live,
+template <class Src, class ShflC, class Probe = NoProbe>
+__device__ __forceinline__ int64_t np_poisson_ptrs_compact(Pcg &g, const PtrsConst &c, const Src &rhs, bool live,
                                                            const PtrsJumpLane &jt, ShflC shfl_c,
                                                            Probe probe = Probe()) {
     const int lane = (int)(threadIdx.x & 63);

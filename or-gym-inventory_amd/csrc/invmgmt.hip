@@ -675,7 +675,7 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
 #ifndef INVSIM_ABL_NO_POISSON
         if (!NPD && P.dist == 1 && P.pc.lam >= 10)   // PTRS with a compacted second round
             dn = np_poisson_ptrs_compact(
-                g, P.pc, [&](int64_t k, const PtrsConst &c) { return ptrs_rhs(c, rhs_l, k); }, true, jt,
+                g, P.pc, RhsTab{rhs_l}, true, jt,
                 [](const PtrsConst &c, int) { return c; });
         else
 #endif

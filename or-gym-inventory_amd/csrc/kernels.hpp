@@ -19,7 +19,7 @@ enum { AR_NEXT_STEP = 0, AR_SAME_STEP = 1, AR_DISABLED = 2 };
 // library): lane 0 of wave b writes s_memrealtime (100 MHz) for probe i to
 // g_tbuf[b][i]; probe 7 holds (XCC_ID << 32) | HW_ID.
 #ifdef INVSIM_TIMING
-constexpr int TB_WAVES = 4096, TB_PROBES = 8;   // probe 7: hardware ids
+constexpr int TB_WAVES = 8192, TB_PROBES = 8;   // probe 7: hardware ids
 #define TPROBE(i)                                                                              \
     do {                                                                                       \
         if (threadIdx.x == 0 && blockIdx.x < TB_WAVES)                                         \
@@ -52,6 +52,7 @@ constexpr int TB_WAVES = 4096, TB_PROBES = 8;   // probe 7: hardware ids
                 ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |                 \
                 (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                           \
             g_tbar[tw_] = 0;                                                                   \
+            g_ttrip[tw_] = 0;                                                                  \
         }                                                                                      \
     } while (0)
 // accumulated barrier wait of each wave (the rollout kernels' workgroup
@@ -64,8 +65,23 @@ static __device__ uint64_t g_tbar[TB_WAVES];
         if ((threadIdx.x & 63) == 0 && tw_ < (unsigned)TB_WAVES)                               \
             g_tbar[tw_] += __builtin_amdgcn_s_memrealtime() - tb0_;                            \
     } while (0)
+// loop trips of each wave (wave-uniform counts added by lane 0), zeroed with g_tbar
+static __device__ uint32_t g_ttrip[TB_WAVES];
+#define TTRIP_ADD(n)                                                                           \
+    do {                                                                                       \
+        const unsigned tw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;                \
+        if ((threadIdx.x & 63) == 0 && tw_ < (unsigned)TB_WAVES) g_ttrip[tw_] += (uint32_t)(n); \
+    } while (0)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
+        v = v > w ? v : w;
+    }
+    return v;
+}
 #define TWAIT() __builtin_amdgcn_s_waitcnt(0)
 #else
+#define TTRIP_ADD(n) do {} while (0)
 #define TBAR_T0() do {} while (0)
 #define TBAR_ADD() do {} while (0)
 #define TPROBE_W(i) do {} while (0)
@@ -212,6 +228,17 @@ __host__ __device__ inline int next_period(int t, int horizon, int autoreset, bo
 
 constexpr int WAVE = 64;          // one-wave workgroups: LDS obs tile stored with 16-B coalesced rows
 constexpr int RHS_LDS_MAX = 512;  // PTRS RHS table entries per Poisson rate (staged in LDS)
+
+struct LgTab {    // loggam(k + 1) for k < RHS_LDS_MAX (Newsvendor's per-episode rate; see RhsTab)
+    const double *lg;
+    __device__ __forceinline__ double fast(int64_t k, const PtrsConst &c, bool &ok) const {
+        ok = k >= 0 && k < RHS_LDS_MAX;
+        return (-c.lam + (double)k * c.loglam) - lg[ok ? (int)k : 0];
+    }
+    __device__ __forceinline__ double exact(int64_t k, const PtrsConst &c) const {
+        return -c.lam + (double)k * c.loglam - np_loggam((double)(k + 1));
+    }
+};
 // Lanes per env.  1 = one thread per env with the sequential sampler; GRP (4) =
 // the lane-group sampler of group_rng.hpp.  tools/poisson_bench.hip measured the
 // sequential sampler (host RHS table + f32 pre-test) 1.1-1.6x faster than the
@@ -343,7 +370,7 @@ __device__ __forceinline__ void roll_wg_sync() {
 // stream exactly as one np_poisson call.
 template <class G>
 __device__ __forceinline__ bool np_poisson_try(G &g, const PtrsConst &c, const double *rhs, int64_t &k) {
-    if (c.lam >= 10) return ptrs_candidate(g, c, [&](int64_t kk, const PtrsConst &cc) { return ptrs_rhs(cc, rhs, kk); }, k);
+    if (c.lam >= 10) return ptrs_candidate(g, c, RhsTab{rhs}, k);   // rhs: an LDS table (never null here)
     k = (c.lam == 0) ? 0 : np_poisson_mult(g, c.enlam);
     return true;
 }

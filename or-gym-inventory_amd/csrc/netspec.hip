@@ -555,7 +555,7 @@ net_step1_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
             const int64_t pd =
                 pc[r].lam >= 10
                     ? np_poisson_ptrs_compact(
-                          g, pc[r], [&](int64_t k, const PtrsConst &c) { return ptrs_rhs(c, rt, k); }, true, jt,
+                          g, pc[r], RhsTab{rt}, true, jt,
                           [](const PtrsConst &c, int) { return c; })
                     : np_poisson(g, pc[r], rt);
             Dd[r] = (double)(pd > 0 ? pd : 0);
@@ -733,7 +733,7 @@ net_step2_kernel(NetParams P, int t, StepIO<float, float> io, int cur, int gla) 
             const int64_t pd =
                 pc[r].lam >= 10
                     ? np_poisson_ptrs_compact(
-                          g, pc[r], [&](int64_t k, const PtrsConst &c) { return ptrs_rhs(c, rt, k); }, true, jt,
+                          g, pc[r], RhsTab{rt}, true, jt,
                           [](const PtrsConst &c, int) { return c; })
                     : np_poisson(g, pc[r], rt);
             Dd[r] = (double)(pd > 0 ? pd : 0);

@@ -605,14 +605,18 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla, i
             }
             const bool mine = mult_wg == (mu < 10 && mu != 0);
             if (!mine) return;
-            PtrsConst c;
+            PtrsConst c;   // the sampler branch's own constants only (PTRS: rows 0-4, else exp(-mu))
             c.lam = mu;
-            c.a = P.pcon[el];
-            c.b = P.pcon[S + el];
-            c.vr = P.pcon[2 * S + el];
-            c.loglam = P.pcon[3 * S + el];
-            c.log_invalpha = P.pcon[4 * S + el];
-            c.enlam = P.pcon[5 * S + el];
+            c.a = c.b = c.vr = c.loglam = c.log_invalpha = c.enlam = 0.0;
+            if (mu >= 10) {
+                c.a = P.pcon[el];
+                c.b = P.pcon[S + el];
+                c.vr = P.pcon[2 * S + el];
+                c.loglam = P.pcon[3 * S + el];
+                c.log_invalpha = P.pcon[4 * S + el];
+            } else {
+                c.enlam = P.pcon[5 * S + el];
+            }
             c.a2 = 2 * c.a;
             c.k0 = 0;
             c.nk = 0;
@@ -636,16 +640,18 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla, i
             }
             const bool mine = mult_wg == (mu < 10 && mu != 0);
             // the chain's constants (nv_rate_const(mu), stored by its first launch),
-            // read only by the lanes whose env this workgroup draws for
+            // read only by the lanes whose env this workgroup draws for, and only
+            // the sampler branch's: PTRS (mu >= 10) rows 0-4, else exp(-mu)
             PtrsConst c;
             c.lam = mu;
             c.a = c.b = c.vr = c.loglam = c.log_invalpha = c.enlam = 0.0;
-            if (mine) {
+            if (mine && mu >= 10) {
                 c.a = P.pcon[el];
                 c.b = P.pcon[S + el];
                 c.vr = P.pcon[2 * S + el];
                 c.loglam = P.pcon[3 * S + el];
                 c.log_invalpha = P.pcon[4 * S + el];
+            } else if (mine) {
                 c.enlam = P.pcon[5 * S + el];
             }
             c.a2 = 2 * c.a;
@@ -658,11 +664,7 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla, i
                 jt.load(lane);
                 const bool live = mine && c.lam >= 10;
                 dn = np_poisson_ptrs_compact(
-                    g, c,
-                    [&](int64_t k, const PtrsConst &cc) {   // as np_poisson_ptrs_lg
-                        return (k < RHS_LDS_MAX) ? (-cc.lam + (double)k * cc.loglam) - lg_l[k < RHS_LDS_MAX ? k : 0]
-                                                 : -cc.lam + (double)k * cc.loglam - np_loggam((double)(k + 1));
-                    },
+                    g, c, LgTab{lg_l},   // as np_poisson_ptrs_lg
                     live, jt,
                     [](const PtrsConst &cc, int src) {
                         PtrsConst r = cc;
@@ -848,6 +850,7 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
     int X = 0;
     double prod = 1.0;
     while (__ballot(j < nd)) {
+        TTRIP_ADD(1);
         const bool live = j < nd;
         uint64_t th, tl;
         mul128(ah, al, s.hi, s.lo, th, tl);
@@ -1097,8 +1100,44 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
 // Chunk c: the stream waves fill it before barrier c, the dynamics wave
 // consumes it between barriers c and c + 1, the obs wave between c + 1 and
 // c + 2 (every wave passes nch + 1 barriers).
+//
+// Round 4, measured and not kept (NV_ROLL_PAIR=1 builds it; parity-green, 306
+// GPU tests): the PTRS stream role on two waves of lane PAIRS, 32 envs each
+// (roles 0 and 4).  A PTRS
+// candidate always consumes exactly two uniforms and its acceptance depends
+// only on them and the episode's rate, so candidate n of an env's stream sits
+// at LCG steps 2n + 1, 2n + 2 whatever the draws before it accepted: the two
+// lanes of a pair evaluate candidates n and n + 1 at once (lane 1 jumps 2 LCG
+// steps ahead, group_rng.hpp), take the accepted ones in stream order and
+// continue from the state after the last candidate consumed -- numpy's draws
+// and end state.  Per chunk a pair needs about half the iterations of one
+// lane, and the two waves run on two SIMDs.  But five waves per workgroup
+// need five waves per SIMD for the grid to stay resident (<= 96 VGPRs: the
+// kernel spills 140 B), and the dispatcher does not balance a workgroup's
+// fifth wave over the SIMDs: a fifth of the workgroups start only when the
+// first ones end (timeline: entry p90 39 us), 29.0 -> 20.4 G env-steps/s
+// (profiles/r04/pair_ab).
+#ifndef NV_ROLL_PAIR
+#define NV_ROLL_PAIR 0
+#endif
+#if defined(INVSIM_NV_FAST_TU) || !NV_ROLL_PAIR
+#define NV_ROLL_WAVES 4
+#define NV_ROLL_BOUNDS __launch_bounds__(4 * WAVE) __attribute__((amdgpu_waves_per_eu(4)))   // <= 128 VGPRs: the grid resident
+#else
+#define NV_ROLL_WAVES 5
+#define NV_ROLL_BOUNDS __launch_bounds__(5 * WAVE) __attribute__((amdgpu_waves_per_eu(5)))
+#endif
+
+// the pair partner's value (lane ^ 1; both lanes of a pair are active together)
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint64_t pair_swap64(uint64_t v) {
+    return ((uint64_t)pair_swap((uint32_t)(v >> 32)) << 32) | pair_swap((uint32_t)v);
+}
+
 template <int LT, bool POL, class RG = Pcg>
-__global__ void __launch_bounds__(4 * WAVE)
+__global__ void NV_ROLL_BOUNDS
 nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     using R = NvRoll<LT>;
     constexpr int O = R::O, CH = R::CH, NP = R::NP;
@@ -1133,13 +1172,17 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     }
     TPROBE_W(0);
     TPROBE_W_ID();
-    if constexpr (!RG::kCounter) if (role < 2) {   // ---- stream waves
+    if constexpr (!RG::kCounter) if (role < 2 || role == 4) {   // ---- stream waves
         const bool multw = role == 1;
-#ifdef NV_ROLL_PRIO
-        if (!multw) __builtin_amdgcn_s_setprio(NV_ROLL_PRIO);   // A/B: the PTRS wave first at issue
-#endif
+        constexpr bool PAIR = NV_ROLL_WAVES == 5;
+        const bool pr = PAIR && !multw;                     // a PTRS pair wave
+        const int o = pr ? (lane & 1) : 0;                  // candidate offset in the pair
+        const int ei = pr ? ((role == 4 ? WAVE / 2 : 0) + (lane >> 1)) : lane;   // env column
+        const int64_t es = e0 + ei;
+        const bool vs = es < N;
+        const int64_t els = vs ? es : N - 1;
         TableStage ts;
-        if (!multw) {
+        if (!multw) {   // both PTRS waves write the whole (identical) table
             ts.dst = lg_l;
             ts.load(P.lgtab, RHS_LDS_MAX, lane);
         } else {
@@ -1147,9 +1190,17 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             for (int q = lane; q < 4 * (JUMP_MAX + 1); q += WAVE) jt[q] = jsrc[q];
         }
         NvState<LT> st;
-        st.g = P.cm.rng.load(el);
-        PtrsConst c = nv_rate_const(P.par[4 * S + el]);
+        st.g = P.cm.rng.load(els);
+        PtrsConst c = nv_rate_const(P.par[4 * S + els]);
         bool mine = nv_mult_branch(c.lam) == multw;
+        // pair lane o: its candidate starts 2o LCG steps past the pair's state
+        // (A_2 s + S_2 inc for o = 1, the identity for o = 0)
+        uint64_t ja_hi = 0, ja_lo = 1, js_hi = 0, js_lo = 0;
+        if (pr && o) {
+            ja_hi = c_jump.a_hi[2];
+            ja_lo = c_jump.a_lo[2];
+            mul128(c_jump.s_hi[2], c_jump.s_lo[2], st.g.inc_hi, st.g.inc_lo, js_hi, js_lo);
+        }
         if (!multw) ts.flush(lane);
         bool reset_any = false;
         int t = t_start, cb = 0;
@@ -1160,8 +1211,8 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             int len;
             bool rs;
             nv_chunk(t, K - k0, P.step_limit, nxt, CH, len, rs);
-            const int nd = mine ? len - (rs ? 1 : 0) : 0;    // draws of this lane (the reset step draws none)
-            int64_t *db = dbuf + cb * CH * WAVE + lane;
+            const int nd = mine ? len - (rs ? 1 : 0) : 0;    // draws of this env (the reset step draws none)
+            int64_t *db = dbuf + cb * CH * WAVE + ei;
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
             for (int j = 0; j < nd; j++) db[j * WAVE] = 20;
 #else
@@ -1174,14 +1225,22 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 for (int j = 0; j < nd; j++) db[j * WAVE] = 5;
             } else
 #endif
-            if (!multw) {
+            if (pr) {
                 if (c.lam == 0) {
-                    for (int j = 0; j < nd; j++) db[j * WAVE] = 0;
+                    if (!o)
+                        for (int j = 0; j < nd; j++) db[j * WAVE] = 0;
                 } else {
-                    // numpy random_poisson_ptrs, one trial per iteration, lanes independent
+                    // numpy random_poisson_ptrs, two candidates per pair and iteration
                     for (int j = 0; j < nd;) {
-                        const double U = st.g.next_double() - 0.5;
-                        const double V = st.g.next_double();
+                        Pcg t = st.g;
+                        {
+                            uint64_t ah, al;
+                            mul128(ja_hi, ja_lo, st.g.hi, st.g.lo, ah, al);
+                            t.lo = al + js_lo;
+                            t.hi = ah + js_hi + (t.lo < al ? 1ULL : 0ULL);
+                        }
+                        const double U = t.next_double() - 0.5;
+                        const double V = t.next_double();
                         const double us = 0.5 - fabs(U);
                         const int64_t kd = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
                         bool acc = (us >= 0.07) && (V <= c.vr);
@@ -1191,11 +1250,57 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                                                  : -c.lam + (double)kd * c.loglam - np_loggam((double)(kd + 1));
                             acc = ptrs_log_accept(c, V, us, r);
                         }
+                        const bool accp = pair_swap(acc ? 1u : 0u) != 0;
+                        const uint64_t ph = pair_swap64(t.hi), pl = pair_swap64(t.lo);
+                        const bool a0 = o ? accp : acc, a1 = o ? acc : accp;
+                        const int j1 = j + (a0 ? 1 : 0);
+                        if (!o && a0) db[j * WAVE] = kd;               // each lane writes its own draw
+                        if (o && a1 && j1 < nd) db[j1 * WAVE] = kd;
+                        const bool stop0 = a0 && j1 == nd;             // candidate n + 1 is not consumed
+                        st.g.hi = (stop0 == (o == 0)) ? t.hi : ph;     // the state after the last one consumed
+                        st.g.lo = (stop0 == (o == 0)) ? t.lo : pl;
+                        j = j1 + ((!stop0 && a1) ? 1 : 0);
+                    }
+                }
+            } else if (!multw) {
+                if (c.lam == 0) {
+                    for (int j = 0; j < nd; j++) db[j * WAVE] = 0;
+                } else {
+                    // numpy random_poisson_ptrs, one trial per iteration, lanes independent
+#ifdef INVSIM_TIMING
+                    uint32_t trips = 0;
+#endif
+                    for (int j = 0; j < nd;) {
+#ifdef INVSIM_TIMING
+                        trips++;
+#endif
+                        const double U = st.g.next_double() - 0.5;
+                        const double V = st.g.next_double();
+                        int64_t kd;
+#if INVSIM_PTRS_DECIDE
+                        const LgTab src{lg_l};
+                        const bool acc = ptrs_decide(
+                            c, U, V, [&](int64_t kk, bool &ok) { return src.fast(kk, c, ok); },
+                            [&](int64_t kk) { return src.exact(kk, c); }, kd);
+#else
+                        const double us = 0.5 - fabs(U);
+                        kd = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+                        bool acc = (us >= 0.07) && (V <= c.vr);
+                        if (!acc && !((kd < 0) || ((us < 0.013) && (V > us)))) {
+                            const double r = (kd < RHS_LDS_MAX)
+                                                 ? (-c.lam + (double)kd * c.loglam) - lg_l[kd < RHS_LDS_MAX ? kd : 0]
+                                                 : -c.lam + (double)kd * c.loglam - np_loggam((double)(kd + 1));
+                            acc = ptrs_log_accept(c, V, us, r);
+                        }
+#endif
                         if (acc) {
                             db[j * WAVE] = kd;
                             j++;
                         }
                     }
+#ifdef INVSIM_TIMING
+                    TTRIP_ADD(wave_max_u32(trips));
+#endif
                 }
             } else if (!nv_mult_chunk_grp(st.g, c.enlam, mine, len - (rs ? 1 : 0), dbuf + cb * CH * WAVE, ubuf, jt, lane)) {
                 // more than 16 envs on this branch: numpy random_poisson_mult, one
@@ -1215,17 +1320,19 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 }
             }
 #endif
-            double *pb = pbuf + cb * NP * WAVE + lane;
+            double *pb = pbuf + cb * NP * WAVE + ei;
 #ifdef INVSIM_TIMING
             if (ci < 4) TPROBE_W(2 + ci);
             ci++;
 #endif
             if (rs && mine) {                      // reset() of the owner: 5 uniforms (:105-111)
-                nv_reset_regs<LT>(P, e, st, nullptr, false);
+                nv_reset_regs<LT>(P, es, st, nullptr, false);
+                if (!o) {
 #pragma unroll
-                for (int j = 0; j < 5; j++) pb[j * WAVE] = st.par[j];
-                pb[5 * WAVE] = __longlong_as_double((long long)st.g.hi);
-                pb[6 * WAVE] = __longlong_as_double((long long)st.g.lo);
+                    for (int j = 0; j < 5; j++) pb[j * WAVE] = st.par[j];
+                    pb[5 * WAVE] = __longlong_as_double((long long)st.g.hi);
+                    pb[6 * WAVE] = __longlong_as_double((long long)st.g.lo);
+                }
             }
             nv_wg_sync();   // barrier: chunk ready
             if (rs) {                              // the new episode's branch owns the generator
@@ -1244,11 +1351,11 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             cb ^= 1;
         }
         nv_wg_sync();   // barrier nch: the obs wave's last chunk
-        if (valid) {
-            if (mine) P.cm.rng.store_state(e, st.g);
+        if (vs && !o) {
+            if (mine) P.cm.rng.store_state(es, st.g);
             if (reset_any && !multw) {
 #pragma unroll
-                for (int j = 0; j < 5; j++) P.par[j * S + e] = st.par[j];
+                for (int j = 0; j < 5; j++) P.par[j * S + es] = st.par[j];
             }
         }
         TWAIT();
@@ -1556,7 +1663,7 @@ hipError_t nv_launch_rg(const NvParams &p, int t_u, const PolicyIO *pol, const S
     }
     if ((!pol || nv_pol_roll_enabled()) && io.K > 1 && t_u >= 0 && p.L > 0 &&
         p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
-        const dim3 gr(grid_for(p.cm.N, WAVE)), br(4 * WAVE);
+        const dim3 gr(grid_for(p.cm.N, WAVE)), br(NV_ROLL_WAVES * WAVE);
         bool done = true;
 #define R_(X)                                                                                              \
     do {                                                                                                   \
@@ -1632,5 +1739,8 @@ extern "C" int invsim_debug_timing_nv(void *dst, int64_t bytes) {
 }
 extern "C" int invsim_debug_timing_bar_nv(void *dst, int64_t bytes) {
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_tbar), (size_t)bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int invsim_debug_timing_trip_nv(void *dst, int64_t bytes) {
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(invsim::g_ttrip), (size_t)bytes, 0, hipMemcpyDeviceToHost);
 }
 #endif

@@ -39,15 +39,15 @@ def main():
             a = torch.floor(torch.rand((K, n, M), device=env.device, generator=g, dtype=torch.float64) * (hi + 1))
             env.rollout(a.to(torch.int64))
     torch.cuda.synchronize()
-    buf = np.zeros((4096, 8), dtype=np.uint64)
+    buf = np.zeros((8192, 8), dtype=np.uint64)
     rc = _capi.lib().invsim_debug_timing(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
     assert rc == 0, rc
-    bar = np.zeros(4096, dtype=np.uint64)
+    bar = np.zeros(8192, dtype=np.uint64)
     rc = _capi.lib().invsim_debug_timing_bar(bar.ctypes.data_as(C.c_void_p), C.c_int64(bar.nbytes))
     assert rc == 0, rc
     R = 3
     W = R * ((n + 63) // 64)
-    assert W <= 4096, "TB_WAVES rows"
+    assert W <= 8192, "TB_WAVES rows"
     b = buf[:W].astype(np.int64)
     bar = bar[:W].astype(np.int64)
     t0 = b[:, 0].min()

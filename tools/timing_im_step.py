@@ -32,7 +32,7 @@ def main():
         a = torch.floor(torch.rand((n, 3), device=env.device, generator=g, dtype=torch.float64) * (hi + 1))
         env.step(a.to(torch.int64))
     torch.cuda.synchronize()
-    buf = np.zeros((4096, 8), dtype=np.uint64)
+    buf = np.zeros((8192, 8), dtype=np.uint64)
     rc = _capi.lib().invsim_debug_timing(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
     assert rc == 0, rc
     b = buf.astype(np.int64)

@@ -1,6 +1,6 @@
-"""Per-wave timeline of the Newsvendor K=30 rollout (nv_roll_kernel, 4 waves
-per 64-env workgroup: PTRS stream wave, multiplication stream wave, dynamics
-wave, obs wave).  Profiling only; needs the TIMING build (csrc `make timing`):
+"""Per-wave timeline of the Newsvendor K=30 rollout (nv_roll_kernel, 5 waves
+per 64-env workgroup: PTRS pair wave A, multiplication stream wave, dynamics
+wave, obs wave, PTRS pair wave B; 4 waves with the NV_ROLL_PAIR=0 build).  Profiling only; needs the TIMING build (csrc `make timing`):
 
   INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so python tools/timing_nv_roll.py
 
@@ -34,17 +34,19 @@ def main():
     for _ in range(4):
         env.rollout(acts)
     torch.cuda.synchronize()
-    buf = np.zeros((4096, 8), dtype=np.uint64)
+    buf = np.zeros((8192, 8), dtype=np.uint64)
     rc = _capi.lib().invsim_debug_timing_nv(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
     assert rc == 0, rc
-    R = 4
+    R = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     W = R * (n // 64)
+    roles = ((0, "PTRS stream"), (1, "mult stream"), (2, "dynamics"), (3, "obs")) + \
+        (((4, "PTRS stream B"),) if R == 5 else ())
     b = buf[:W].astype(np.int64)
     t0 = b[:, 0].min()
     pct = [0, 10, 50, 90, 100]
     fmt = lambda x: " ".join(f"{v * 10.0:8.0f}" for v in np.percentile(x, pct))  # noqa: E731
     print("ns percentiles        p0       p10      p50      p90      max")
-    for role, name in ((0, "PTRS stream"), (1, "mult stream"), (2, "dynamics"), (3, "obs")):
+    for role, name in roles:
         sel = b[role::R]
         print(f"-- {name}: {len(sel)} waves")
         print("  entry          " + fmt(sel[:, 0] - t0))
@@ -56,8 +58,10 @@ def main():
         print("  exit           " + fmt(sel[:, 6] - t0))
     # per chunk: how long the dynamics wave waited at the barrier for its stream waves
     d, p, m = b[2::R], b[0::R], b[1::R]
+    if R == 5:
+        p = np.maximum(p, b[4::R])
     for c in range(3):
-        ready = np.maximum(p[:, 3 + c], m[:, 3 + c])          # chunk c+1 drawn by both stream waves
+        ready = np.maximum(p[:, 3 + c], m[:, 3 + c])          # chunk c+1 drawn by the stream waves
         wait = np.maximum(0, ready - d[:, 2 + c])
         print(f"barrier {c + 1}: dynamics waits for the stream waves  " + fmt(wait))
     # SIMD sharing: waves per (XCC, SE, CU, SIMD)
@@ -76,15 +80,28 @@ def main():
     print("workgroups with all %d waves on one SIMD: %.1f %%" % (R, 100.0 * same))
     share = np.array([np.sum(ptrs_key == k) for k in ptrs_key])
     print("PTRS waves sharing their SIMD with another PTRS wave: %.1f %%" % (100.0 * np.mean(share > 1)))
-    bar = np.zeros(4096, dtype=np.uint64)
+    bar = np.zeros(8192, dtype=np.uint64)
     rc = _capi.lib().invsim_debug_timing_bar_nv(bar.ctypes.data_as(C.c_void_p), C.c_int64(bar.nbytes))
     assert rc == 0, rc
     bar = bar[:W].astype(np.int64)
     print("per role (last launch): lifetime = exit - entry, barrier wait, work = lifetime - wait")
-    for role, name in ((0, "PTRS stream"), (1, "mult stream"), (2, "dynamics"), (3, "obs")):
+    for role, name in roles:
         life = b[role::R, 6] - b[role::R, 0]
         wt = bar[role::R]
         print(f"  {name:12s} life {fmt(life)}\n  {'':12s} wait {fmt(wt)}\n  {'':12s} work {fmt(life - wt)}")
+    trip = np.zeros(8192, dtype=np.uint32)
+    if hasattr(_capi.lib(), "invsim_debug_timing_trip_nv"):
+        rc = _capi.lib().invsim_debug_timing_trip_nv(trip.ctypes.data_as(C.c_void_p), C.c_int64(trip.nbytes))
+        assert rc == 0, rc
+        trip = trip[:W].astype(np.int64)
+        print("loop trips per wave (PTRS: the per-chunk max over lanes, summed; mult: rounds) and work per trip")
+        for role, name in ((0, "PTRS stream"), (1, "mult stream")):
+            tr = trip[role::R]
+            life = b[role::R, 6] - b[role::R, 0]
+            work = life - bar[role::R]
+            ok = tr > 0
+            print(f"  {name:12s} trips {fmt(tr / 10.0)}")
+            print(f"  {'':12s} ns/trip {fmt(work[ok] / tr[ok])}")
     print(f"kernel span {(b[:, 6].max() - t0) * 10.0:.0f} ns")
 
 

@@ -29,7 +29,7 @@ def main():
     for _ in range(12):
         env.step(torch.rand((n, 1), device=env.device, generator=g) * 400)
     torch.cuda.synchronize()
-    buf = np.zeros((4096, 8), dtype=np.uint64)
+    buf = np.zeros((8192, 8), dtype=np.uint64)
     rc = _capi.lib().invsim_debug_timing_nv(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
     assert rc == 0, rc
     b = buf.astype(np.int64)

@@ -45,8 +45,8 @@ def main():
         env.step(a)
     torch.cuda.synchronize()
     lib = _capi.lib()
-    waves = min((args.n + 63) // 64, 4096)
-    buf = np.zeros((4096, 8), dtype=np.uint64)
+    waves = min((args.n + 63) // 64, 8192)
+    buf = np.zeros((8192, 8), dtype=np.uint64)
     fn = lib.invsim_debug_timing_nv if args.newsvendor else lib.invsim_debug_timing
     rc = fn(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
     assert rc == 0, rc
