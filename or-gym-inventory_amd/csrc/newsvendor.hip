@@ -1101,32 +1101,36 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
 // consumes it between barriers c and c + 1, the obs wave between c + 1 and
 // c + 2 (every wave passes nch + 1 barriers).
 //
-// Round 4, measured and not kept (NV_ROLL_PAIR=1 builds it; parity-green, 306
-// GPU tests): the PTRS stream role on two waves of lane PAIRS, 32 envs each
-// (roles 0 and 4).  A PTRS
-// candidate always consumes exactly two uniforms and its acceptance depends
-// only on them and the episode's rate, so candidate n of an env's stream sits
-// at LCG steps 2n + 1, 2n + 2 whatever the draws before it accepted: the two
-// lanes of a pair evaluate candidates n and n + 1 at once (lane 1 jumps 2 LCG
-// steps ahead, group_rng.hpp), take the accepted ones in stream order and
-// continue from the state after the last candidate consumed -- numpy's draws
-// and end state.  Per chunk a pair needs about half the iterations of one
-// lane, and the two waves run on two SIMDs.  But five waves per workgroup
-// need five waves per SIMD for the grid to stay resident (<= 96 VGPRs: the
-// kernel spills 140 B), and the dispatcher does not balance a workgroup's
-// fifth wave over the SIMDs: a fifth of the workgroups start only when the
-// first ones end (timeline: entry p90 39 us), 29.0 -> 20.4 G env-steps/s
-// (profiles/r04/pair_ab).
-#ifndef NV_ROLL_PAIR
-#define NV_ROLL_PAIR 0
+// Round 4, layout 1 (NV_ROLL_LAYOUT, the default for the parity stream): the
+// PTRS role on two waves of lane PAIRS, 32 envs each, and the multiplication
+// branch's draws moved into the obs wave:
+//   waves 0, 1 (PTRS pairs)  envs 32 w .. 32 w + 31, two lanes per env.  A PTRS
+//                            candidate always consumes exactly two uniforms and
+//                            its acceptance depends only on them and the
+//                            episode's rate, so candidate n of an env's stream
+//                            sits at LCG steps 2n + 1, 2n + 2 whatever the draws
+//                            before it accepted: the lanes of a pair evaluate
+//                            candidates n and n + 1 at once (lane 1 jumps two
+//                            LCG steps ahead, group_rng.hpp), take the accepted
+//                            ones in stream order and continue from the state
+//                            after the last candidate consumed -- numpy's draws
+//                            and end state, in about half the trips per chunk
+//   wave 2 (dynamics)        as above
+//   wave 3 (obs + mult)      draws chunk b of the multiplication-branch envs
+//                            (nv_mult_chunk_grp) and builds the observations of
+//                            chunk b - 2 before barrier b
+// A PTRS wave trip is one wave's issue-bound instruction chain (~1 us), so
+// halving the trips is what shortens the launch; the obs wave had the spare
+// issue slots for the multiplication draws.  Layout 0 keeps one PTRS wave and
+// a multiplication wave.  (A 5-wave variant with the pairs beside the
+// multiplication wave, commit 05546b1, measured slower: five waves per SIMD
+// need <= 96 VGPRs, and the dispatcher does not spread a workgroup's fifth
+// wave evenly, so a fifth of the grid started late; profiles/r04/pair_ab.)
+#ifndef NV_ROLL_LAYOUT
+#define NV_ROLL_LAYOUT 1
 #endif
-#if defined(INVSIM_NV_FAST_TU) || !NV_ROLL_PAIR
 #define NV_ROLL_WAVES 4
 #define NV_ROLL_BOUNDS __launch_bounds__(4 * WAVE) __attribute__((amdgpu_waves_per_eu(4)))   // <= 128 VGPRs: the grid resident
-#else
-#define NV_ROLL_WAVES 5
-#define NV_ROLL_BOUNDS __launch_bounds__(5 * WAVE) __attribute__((amdgpu_waves_per_eu(5)))
-#endif
 
 // the pair partner's value (lane ^ 1; both lanes of a pair are active together)
 __device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
@@ -1172,12 +1176,12 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     }
     TPROBE_W(0);
     TPROBE_W_ID();
-    if constexpr (!RG::kCounter) if (role < 2 || role == 4) {   // ---- stream waves
-        const bool multw = role == 1;
-        constexpr bool PAIR = NV_ROLL_WAVES == 5;
-        const bool pr = PAIR && !multw;                     // a PTRS pair wave
+    constexpr bool L1 = NV_ROLL_LAYOUT == 1 && !RG::kCounter;
+    if constexpr (!RG::kCounter) if (role < 2) {   // ---- stream waves (layout 1: the two PTRS pair waves)
+        const bool multw = !L1 && role == 1;
+        const bool pr = L1;                                  // a PTRS pair wave
         const int o = pr ? (lane & 1) : 0;                  // candidate offset in the pair
-        const int ei = pr ? ((role == 4 ? WAVE / 2 : 0) + (lane >> 1)) : lane;   // env column
+        const int ei = pr ? (role * (WAVE / 2) + (lane >> 1)) : lane;   // env column
         const int64_t es = e0 + ei;
         const bool vs = es < N;
         const int64_t els = vs ? es : N - 1;
@@ -1231,7 +1235,13 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                         for (int j = 0; j < nd; j++) db[j * WAVE] = 0;
                 } else {
                     // numpy random_poisson_ptrs, two candidates per pair and iteration
+#ifdef INVSIM_TIMING
+                    uint32_t trips = 0;
+#endif
                     for (int j = 0; j < nd;) {
+#ifdef INVSIM_TIMING
+                        trips++;
+#endif
                         Pcg t = st.g;
                         {
                             uint64_t ah, al;
@@ -1261,6 +1271,9 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                         st.g.lo = (stop0 == (o == 0)) ? t.lo : pl;
                         j = j1 + ((!stop0 && a1) ? 1 : 0);
                     }
+#ifdef INVSIM_TIMING
+                    TTRIP_ADD(wave_max_u32(trips));
+#endif
                 }
             } else if (!multw) {
                 if (c.lam == 0) {
@@ -1362,7 +1375,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
         TPROBE_W(6);
         return;
     }
-    if (role == 3) {   // ---- obs wave
+    if (role == 3) {   // ---- obs wave (layout 1: + the multiplication-branch draws)
         float *trow = tile + lane * O;
         int sc = t_start;
         float pf[5], pv[LT];
@@ -1380,13 +1393,9 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
         }
 #pragma unroll
         for (int j = 0; j < 5; j++) trow[j] = pf[j];   // the params part changes only at a reset
-        int kk = 0, cb = 0;
-        nv_wg_sync();   // barrier 0
-        nv_wg_sync();   // barrier 1: chunk 0 handed over
-        TPROBE_W(1);
-        int ci = 0;
-        (void)ci;
-        for (int k = 0; k < K; k++) {
+        // the observation, reward and flags of launch step k (step kk of the chunk
+        // in handoff buffer cb); returns whether it was a reset step
+        auto obs_step = [&](int k, int kk, int cb) -> bool {
             const int64_t oi = (int64_t)k * N + e;
             const bool rs = nxt && sc >= P.step_limit;
             double r = 0.0;
@@ -1421,15 +1430,100 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             if (!POL || io.obs) store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
 #endif
             wave_lds_sync();
-            if (++kk == CH || rs || k == K - 1) {      // chunk consumed
+            return rs;
+        };
+        if constexpr (!L1) {
+            int kk = 0, cb = 0;
+            nv_wg_sync();   // barrier 0
+            nv_wg_sync();   // barrier 1: chunk 0 handed over
+            TPROBE_W(1);
+            int ci = 0;
+            (void)ci;
+            for (int k = 0; k < K; k++) {
+                const bool rs = obs_step(k, kk, cb);
+                if (++kk == CH || rs || k == K - 1) {      // chunk consumed
 #ifdef INVSIM_TIMING
-                if (ci < 4) TPROBE_W(2 + ci);
-                ci++;
+                    if (ci < 4) TPROBE_W(2 + ci);
+                    ci++;
 #endif
-                if (k + 1 < K) nv_wg_sync();             // barrier of the next chunk's handoff
-                kk = 0;
+                    if (k + 1 < K) nv_wg_sync();             // barrier of the next chunk's handoff
+                    kk = 0;
+                    cb ^= 1;
+                }
+            }
+        } else {
+            int ko = 0, cbo = 0;
+            auto obs_chunk = [&]() {                     // the next chunk's observations
+                for (int kk = 0;;) {
+                    const bool rs = obs_step(ko, kk, cbo);
+                    ko++;
+                    if (++kk == CH || rs || ko == K) break;
+                }
+                cbo ^= 1;
+            };
+            // the multiplication-branch stream (layout 0's wave 1), one env per lane:
+            // it owns the generators of the envs whose episode rate is 0 < mu < 10
+            {
+                const uint64_t *jsrc = &c_jump.a_hi[0];   // the four rows are contiguous
+                for (int q = lane; q < 4 * (JUMP_MAX + 1); q += WAVE) jt[q] = jsrc[q];
+            }
+            NvState<LT> sm;
+            sm.g = P.cm.rng.load(el);
+            double mu = P.par[4 * S + el];
+            double enlam = exp(-mu);                        // nv_rate_const's exp(-lam)
+            bool mine = nv_mult_branch(mu);
+            int tm = t_start, k0 = 0, cb = 0, b = 0;
+            TPROBE_W(1);
+            for (; k0 < K; b++) {
+                if (b >= 2) obs_chunk();                    // chunk b - 2 (handed over at barrier b - 1)
+                int len;
+                bool rs;
+                nv_chunk(tm, K - k0, P.step_limit, nxt, CH, len, rs);
+                const int nd = mine ? len - (rs ? 1 : 0) : 0;
+                int64_t *db = dbuf + cb * CH * WAVE + lane;
+                if (!nv_mult_chunk_grp(sm.g, enlam, mine, len - (rs ? 1 : 0), dbuf + cb * CH * WAVE, ubuf, jt, lane)) {
+                    // more than 16 envs on this branch: numpy random_poisson_mult, one
+                    // uniform per iteration, lanes independent
+                    int64_t X = 0;
+                    double prod = 1.0;
+                    for (int j = 0; j < nd;) {
+                        prod *= sm.g.next_double();
+                        if (prod > enlam) {
+                            X += 1;
+                        } else {
+                            db[j * WAVE] = X;
+                            j++;
+                            X = 0;
+                            prod = 1.0;
+                        }
+                    }
+                }
+                double *pb = pbuf + cb * NP * WAVE + lane;
+                if (rs && mine) {                           // reset() of the owner: 5 uniforms (:105-111)
+                    nv_reset_regs<LT>(P, e, sm, nullptr, false);
+#pragma unroll
+                    for (int j = 0; j < 5; j++) pb[j * WAVE] = sm.par[j];
+                    pb[5 * WAVE] = __longlong_as_double((long long)sm.g.hi);
+                    pb[6 * WAVE] = __longlong_as_double((long long)sm.g.lo);
+                }
+                nv_wg_sync();   // barrier b: chunk b ready
+                if (rs) {                                   // the new episode's branch owns the generator
+                    mu = pb[4 * WAVE];
+                    sm.g.hi = (uint64_t)__double_as_longlong(pb[5 * WAVE]);
+                    sm.g.lo = (uint64_t)__double_as_longlong(pb[6 * WAVE]);
+                    enlam = exp(-mu);
+                    mine = nv_mult_branch(mu);
+                    tm = 0;
+                } else {
+                    tm += len;
+                }
+                k0 += len;
                 cb ^= 1;
             }
+            if (b >= 2) obs_chunk();   // chunk nch - 2
+            nv_wg_sync();              // barrier nch
+            obs_chunk();               // chunk nch - 1
+            if (valid && mine) P.cm.rng.store_state(e, sm.g);
         }
         TWAIT();
         TPROBE_W(6);

@@ -1,8 +1,9 @@
-"""Per-wave timeline of the Newsvendor K=30 rollout (nv_roll_kernel, 5 waves
-per 64-env workgroup: PTRS pair wave A, multiplication stream wave, dynamics
-wave, obs wave, PTRS pair wave B; 4 waves with the NV_ROLL_PAIR=0 build).  Profiling only; needs the TIMING build (csrc `make timing`):
+"""Per-wave timeline of the Newsvendor K=30 rollout (nv_roll_kernel, 4 waves
+per 64-env workgroup; layout L1: two PTRS lane-pair waves, dynamics wave, obs
+wave with the multiplication-branch draws; L0 (NV_ROLL_LAYOUT=0): PTRS wave,
+multiplication wave, dynamics wave, obs wave).  Profiling only; needs the TIMING build (csrc `make timing`):
 
-  INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so python tools/timing_nv_roll.py
+  INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so python tools/timing_nv_roll.py [L1|L0]
 
 Probes (s_memrealtime, 100 MHz, lane 0 of every wave, row = workgroup * 4 +
 wave): 0 entry, 1 ready (stream: state + tables loaded; dynamics: barrier 0
@@ -37,10 +38,15 @@ def main():
     buf = np.zeros((8192, 8), dtype=np.uint64)
     rc = _capi.lib().invsim_debug_timing_nv(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
     assert rc == 0, rc
-    R = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    layout = sys.argv[1] if len(sys.argv) > 1 else "L1"   # L1: PTRS pairs + obs/mult wave; L0: the round-4 4-role kernel
+    R = 4
     W = R * (n // 64)
-    roles = ((0, "PTRS stream"), (1, "mult stream"), (2, "dynamics"), (3, "obs")) + \
-        (((4, "PTRS stream B"),) if R == 5 else ())
+    if layout == "L1":
+        roles = ((0, "PTRS pairs A"), (1, "PTRS pairs B"), (2, "dynamics"), (3, "obs + mult"))
+        trip_roles = ((0, "PTRS pairs A"), (1, "PTRS pairs B"), (3, "obs + mult"))
+    else:
+        roles = ((0, "PTRS stream"), (1, "mult stream"), (2, "dynamics"), (3, "obs"))
+        trip_roles = ((0, "PTRS stream"), (1, "mult stream"))
     b = buf[:W].astype(np.int64)
     t0 = b[:, 0].min()
     pct = [0, 10, 50, 90, 100]
@@ -58,9 +64,7 @@ def main():
         print("  exit           " + fmt(sel[:, 6] - t0))
     # per chunk: how long the dynamics wave waited at the barrier for its stream waves
     d, p, m = b[2::R], b[0::R], b[1::R]
-    if R == 5:
-        p = np.maximum(p, b[4::R])
-    for c in range(3):
+    for c in range(3 if layout == "L0" else 0):
         ready = np.maximum(p[:, 3 + c], m[:, 3 + c])          # chunk c+1 drawn by the stream waves
         wait = np.maximum(0, ready - d[:, 2 + c])
         print(f"barrier {c + 1}: dynamics waits for the stream waves  " + fmt(wait))
@@ -95,7 +99,7 @@ def main():
         assert rc == 0, rc
         trip = trip[:W].astype(np.int64)
         print("loop trips per wave (PTRS: the per-chunk max over lanes, summed; mult: rounds) and work per trip")
-        for role, name in ((0, "PTRS stream"), (1, "mult stream")):
+        for role, name in trip_roles:
             tr = trip[role::R]
             life = b[role::R, 6] - b[role::R, 0]
             work = life - bar[role::R]
