@@ -1101,44 +1101,17 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
 // consumes it between barriers c and c + 1, the obs wave between c + 1 and
 // c + 2 (every wave passes nch + 1 barriers).
 //
-// Round 4, layout 1 (NV_ROLL_LAYOUT, the default for the parity stream): the
-// PTRS role on two waves of lane PAIRS, 32 envs each, and the multiplication
-// branch's draws moved into the obs wave:
-//   waves 0, 1 (PTRS pairs)  envs 32 w .. 32 w + 31, two lanes per env.  A PTRS
-//                            candidate always consumes exactly two uniforms and
-//                            its acceptance depends only on them and the
-//                            episode's rate, so candidate n of an env's stream
-//                            sits at LCG steps 2n + 1, 2n + 2 whatever the draws
-//                            before it accepted: the lanes of a pair evaluate
-//                            candidates n and n + 1 at once (lane 1 jumps two
-//                            LCG steps ahead, group_rng.hpp), take the accepted
-//                            ones in stream order and continue from the state
-//                            after the last candidate consumed -- numpy's draws
-//                            and end state, in about half the trips per chunk
-//   wave 2 (dynamics)        as above
-//   wave 3 (obs + mult)      draws chunk b of the multiplication-branch envs
-//                            (nv_mult_chunk_grp) and builds the observations of
-//                            chunk b - 2 before barrier b
-// A PTRS wave trip is one wave's issue-bound instruction chain (~1 us), so
-// halving the trips is what shortens the launch; the obs wave had the spare
-// issue slots for the multiplication draws.  Layout 0 keeps one PTRS wave and
-// a multiplication wave.  (A 5-wave variant with the pairs beside the
-// multiplication wave, commit 05546b1, measured slower: five waves per SIMD
-// need <= 96 VGPRs, and the dispatcher does not spread a workgroup's fifth
-// wave evenly, so a fifth of the grid started late; profiles/r04/pair_ab.)
-#ifndef NV_ROLL_LAYOUT
-#define NV_ROLL_LAYOUT 1
-#endif
+// Measured and not kept in round 4 (profiles/r04/pair_ab, layout_ab): the
+// PTRS role on lane PAIRS (a PTRS candidate always consumes two uniforms and
+// its acceptance depends only on them and the rate, so the two lanes of a pair
+// can evaluate candidates n and n + 1 at once, lane 1 jumping two LCG steps
+// ahead, and take the accepted ones in stream order -- numpy's draws, half the
+// trips per chunk).  As a fifth wave (commit 05546b1) the grid no longer fits
+// at once (<= 96 VGPRs, uneven placement of the fifth wave): 29.0 -> 20.4 G.
+// As two pair waves with the multiplication draws moved into the obs wave
+// (commit b4c9eaf) the obs wave became the tail: 29.3 -> 26.0 G.
 #define NV_ROLL_WAVES 4
 #define NV_ROLL_BOUNDS __launch_bounds__(4 * WAVE) __attribute__((amdgpu_waves_per_eu(4)))   // <= 128 VGPRs: the grid resident
-
-// the pair partner's value (lane ^ 1; both lanes of a pair are active together)
-__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-}
-__device__ __forceinline__ uint64_t pair_swap64(uint64_t v) {
-    return ((uint64_t)pair_swap((uint32_t)(v >> 32)) << 32) | pair_swap((uint32_t)v);
-}
 
 template <int LT, bool POL, class RG = Pcg>
 __global__ void NV_ROLL_BOUNDS
@@ -1176,17 +1149,10 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     }
     TPROBE_W(0);
     TPROBE_W_ID();
-    constexpr bool L1 = NV_ROLL_LAYOUT == 1 && !RG::kCounter;
-    if constexpr (!RG::kCounter) if (role < 2) {   // ---- stream waves (layout 1: the two PTRS pair waves)
-        const bool multw = !L1 && role == 1;
-        const bool pr = L1;                                  // a PTRS pair wave
-        const int o = pr ? (lane & 1) : 0;                  // candidate offset in the pair
-        const int ei = pr ? (role * (WAVE / 2) + (lane >> 1)) : lane;   // env column
-        const int64_t es = e0 + ei;
-        const bool vs = es < N;
-        const int64_t els = vs ? es : N - 1;
+    if constexpr (!RG::kCounter) if (role < 2) {   // ---- stream waves
+        const bool multw = role == 1;
         TableStage ts;
-        if (!multw) {   // both PTRS waves write the whole (identical) table
+        if (!multw) {
             ts.dst = lg_l;
             ts.load(P.lgtab, RHS_LDS_MAX, lane);
         } else {
@@ -1194,17 +1160,9 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             for (int q = lane; q < 4 * (JUMP_MAX + 1); q += WAVE) jt[q] = jsrc[q];
         }
         NvState<LT> st;
-        st.g = P.cm.rng.load(els);
-        PtrsConst c = nv_rate_const(P.par[4 * S + els]);
+        st.g = P.cm.rng.load(el);
+        PtrsConst c = nv_rate_const(P.par[4 * S + el]);
         bool mine = nv_mult_branch(c.lam) == multw;
-        // pair lane o: its candidate starts 2o LCG steps past the pair's state
-        // (A_2 s + S_2 inc for o = 1, the identity for o = 0)
-        uint64_t ja_hi = 0, ja_lo = 1, js_hi = 0, js_lo = 0;
-        if (pr && o) {
-            ja_hi = c_jump.a_hi[2];
-            ja_lo = c_jump.a_lo[2];
-            mul128(c_jump.s_hi[2], c_jump.s_lo[2], st.g.inc_hi, st.g.inc_lo, js_hi, js_lo);
-        }
         if (!multw) ts.flush(lane);
         bool reset_any = false;
         int t = t_start, cb = 0;
@@ -1216,7 +1174,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             bool rs;
             nv_chunk(t, K - k0, P.step_limit, nxt, CH, len, rs);
             const int nd = mine ? len - (rs ? 1 : 0) : 0;    // draws of this env (the reset step draws none)
-            int64_t *db = dbuf + cb * CH * WAVE + ei;
+            int64_t *db = dbuf + cb * CH * WAVE + lane;
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
             for (int j = 0; j < nd; j++) db[j * WAVE] = 20;
 #else
@@ -1229,53 +1187,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 for (int j = 0; j < nd; j++) db[j * WAVE] = 5;
             } else
 #endif
-            if (pr) {
-                if (c.lam == 0) {
-                    if (!o)
-                        for (int j = 0; j < nd; j++) db[j * WAVE] = 0;
-                } else {
-                    // numpy random_poisson_ptrs, two candidates per pair and iteration
-#ifdef INVSIM_TIMING
-                    uint32_t trips = 0;
-#endif
-                    for (int j = 0; j < nd;) {
-#ifdef INVSIM_TIMING
-                        trips++;
-#endif
-                        Pcg t = st.g;
-                        {
-                            uint64_t ah, al;
-                            mul128(ja_hi, ja_lo, st.g.hi, st.g.lo, ah, al);
-                            t.lo = al + js_lo;
-                            t.hi = ah + js_hi + (t.lo < al ? 1ULL : 0ULL);
-                        }
-                        const double U = t.next_double() - 0.5;
-                        const double V = t.next_double();
-                        const double us = 0.5 - fabs(U);
-                        const int64_t kd = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
-                        bool acc = (us >= 0.07) && (V <= c.vr);
-                        if (!acc && !((kd < 0) || ((us < 0.013) && (V > us)))) {
-                            const double r = (kd < RHS_LDS_MAX)
-                                                 ? (-c.lam + (double)kd * c.loglam) - lg_l[kd < RHS_LDS_MAX ? kd : 0]
-                                                 : -c.lam + (double)kd * c.loglam - np_loggam((double)(kd + 1));
-                            acc = ptrs_log_accept(c, V, us, r);
-                        }
-                        const bool accp = pair_swap(acc ? 1u : 0u) != 0;
-                        const uint64_t ph = pair_swap64(t.hi), pl = pair_swap64(t.lo);
-                        const bool a0 = o ? accp : acc, a1 = o ? acc : accp;
-                        const int j1 = j + (a0 ? 1 : 0);
-                        if (!o && a0) db[j * WAVE] = kd;               // each lane writes its own draw
-                        if (o && a1 && j1 < nd) db[j1 * WAVE] = kd;
-                        const bool stop0 = a0 && j1 == nd;             // candidate n + 1 is not consumed
-                        st.g.hi = (stop0 == (o == 0)) ? t.hi : ph;     // the state after the last one consumed
-                        st.g.lo = (stop0 == (o == 0)) ? t.lo : pl;
-                        j = j1 + ((!stop0 && a1) ? 1 : 0);
-                    }
-#ifdef INVSIM_TIMING
-                    TTRIP_ADD(wave_max_u32(trips));
-#endif
-                }
-            } else if (!multw) {
+            if (!multw) {
                 if (c.lam == 0) {
                     for (int j = 0; j < nd; j++) db[j * WAVE] = 0;
                 } else {
@@ -1333,19 +1245,17 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 }
             }
 #endif
-            double *pb = pbuf + cb * NP * WAVE + ei;
+            double *pb = pbuf + cb * NP * WAVE + lane;
 #ifdef INVSIM_TIMING
             if (ci < 4) TPROBE_W(2 + ci);
             ci++;
 #endif
             if (rs && mine) {                      // reset() of the owner: 5 uniforms (:105-111)
-                nv_reset_regs<LT>(P, es, st, nullptr, false);
-                if (!o) {
+                nv_reset_regs<LT>(P, e, st, nullptr, false);
 #pragma unroll
-                    for (int j = 0; j < 5; j++) pb[j * WAVE] = st.par[j];
-                    pb[5 * WAVE] = __longlong_as_double((long long)st.g.hi);
-                    pb[6 * WAVE] = __longlong_as_double((long long)st.g.lo);
-                }
+                for (int j = 0; j < 5; j++) pb[j * WAVE] = st.par[j];
+                pb[5 * WAVE] = __longlong_as_double((long long)st.g.hi);
+                pb[6 * WAVE] = __longlong_as_double((long long)st.g.lo);
             }
             nv_wg_sync();   // barrier: chunk ready
             if (rs) {                              // the new episode's branch owns the generator
@@ -1364,18 +1274,18 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             cb ^= 1;
         }
         nv_wg_sync();   // barrier nch: the obs wave's last chunk
-        if (vs && !o) {
-            if (mine) P.cm.rng.store_state(es, st.g);
+        if (valid) {
+            if (mine) P.cm.rng.store_state(e, st.g);
             if (reset_any && !multw) {
 #pragma unroll
-                for (int j = 0; j < 5; j++) P.par[j * S + es] = st.par[j];
+                for (int j = 0; j < 5; j++) P.par[j * S + e] = st.par[j];
             }
         }
         TWAIT();
         TPROBE_W(6);
         return;
     }
-    if (role == 3) {   // ---- obs wave (layout 1: + the multiplication-branch draws)
+    if (role == 3) {   // ---- obs wave
         float *trow = tile + lane * O;
         int sc = t_start;
         float pf[5], pv[LT];
@@ -1432,98 +1342,23 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             wave_lds_sync();
             return rs;
         };
-        if constexpr (!L1) {
-            int kk = 0, cb = 0;
-            nv_wg_sync();   // barrier 0
-            nv_wg_sync();   // barrier 1: chunk 0 handed over
-            TPROBE_W(1);
-            int ci = 0;
-            (void)ci;
-            for (int k = 0; k < K; k++) {
-                const bool rs = obs_step(k, kk, cb);
-                if (++kk == CH || rs || k == K - 1) {      // chunk consumed
+        int kk = 0, cb = 0;
+        nv_wg_sync();   // barrier 0
+        nv_wg_sync();   // barrier 1: chunk 0 handed over
+        TPROBE_W(1);
+        int ci = 0;
+        (void)ci;
+        for (int k = 0; k < K; k++) {
+            const bool rs = obs_step(k, kk, cb);
+            if (++kk == CH || rs || k == K - 1) {      // chunk consumed
 #ifdef INVSIM_TIMING
-                    if (ci < 4) TPROBE_W(2 + ci);
-                    ci++;
+                if (ci < 4) TPROBE_W(2 + ci);
+                ci++;
 #endif
-                    if (k + 1 < K) nv_wg_sync();             // barrier of the next chunk's handoff
-                    kk = 0;
-                    cb ^= 1;
-                }
-            }
-        } else {
-            int ko = 0, cbo = 0;
-            auto obs_chunk = [&]() {                     // the next chunk's observations
-                for (int kk = 0;;) {
-                    const bool rs = obs_step(ko, kk, cbo);
-                    ko++;
-                    if (++kk == CH || rs || ko == K) break;
-                }
-                cbo ^= 1;
-            };
-            // the multiplication-branch stream (layout 0's wave 1), one env per lane:
-            // it owns the generators of the envs whose episode rate is 0 < mu < 10
-            {
-                const uint64_t *jsrc = &c_jump.a_hi[0];   // the four rows are contiguous
-                for (int q = lane; q < 4 * (JUMP_MAX + 1); q += WAVE) jt[q] = jsrc[q];
-            }
-            NvState<LT> sm;
-            sm.g = P.cm.rng.load(el);
-            double mu = P.par[4 * S + el];
-            double enlam = exp(-mu);                        // nv_rate_const's exp(-lam)
-            bool mine = nv_mult_branch(mu);
-            int tm = t_start, k0 = 0, cb = 0, b = 0;
-            TPROBE_W(1);
-            for (; k0 < K; b++) {
-                if (b >= 2) obs_chunk();                    // chunk b - 2 (handed over at barrier b - 1)
-                int len;
-                bool rs;
-                nv_chunk(tm, K - k0, P.step_limit, nxt, CH, len, rs);
-                const int nd = mine ? len - (rs ? 1 : 0) : 0;
-                int64_t *db = dbuf + cb * CH * WAVE + lane;
-                if (!nv_mult_chunk_grp(sm.g, enlam, mine, len - (rs ? 1 : 0), dbuf + cb * CH * WAVE, ubuf, jt, lane)) {
-                    // more than 16 envs on this branch: numpy random_poisson_mult, one
-                    // uniform per iteration, lanes independent
-                    int64_t X = 0;
-                    double prod = 1.0;
-                    for (int j = 0; j < nd;) {
-                        prod *= sm.g.next_double();
-                        if (prod > enlam) {
-                            X += 1;
-                        } else {
-                            db[j * WAVE] = X;
-                            j++;
-                            X = 0;
-                            prod = 1.0;
-                        }
-                    }
-                }
-                double *pb = pbuf + cb * NP * WAVE + lane;
-                if (rs && mine) {                           // reset() of the owner: 5 uniforms (:105-111)
-                    nv_reset_regs<LT>(P, e, sm, nullptr, false);
-#pragma unroll
-                    for (int j = 0; j < 5; j++) pb[j * WAVE] = sm.par[j];
-                    pb[5 * WAVE] = __longlong_as_double((long long)sm.g.hi);
-                    pb[6 * WAVE] = __longlong_as_double((long long)sm.g.lo);
-                }
-                nv_wg_sync();   // barrier b: chunk b ready
-                if (rs) {                                   // the new episode's branch owns the generator
-                    mu = pb[4 * WAVE];
-                    sm.g.hi = (uint64_t)__double_as_longlong(pb[5 * WAVE]);
-                    sm.g.lo = (uint64_t)__double_as_longlong(pb[6 * WAVE]);
-                    enlam = exp(-mu);
-                    mine = nv_mult_branch(mu);
-                    tm = 0;
-                } else {
-                    tm += len;
-                }
-                k0 += len;
+                if (k + 1 < K) nv_wg_sync();             // barrier of the next chunk's handoff
+                kk = 0;
                 cb ^= 1;
             }
-            if (b >= 2) obs_chunk();   // chunk nch - 2
-            nv_wg_sync();              // barrier nch
-            obs_chunk();               // chunk nch - 1
-            if (valid && mine) P.cm.rng.store_state(e, sm.g);
         }
         TWAIT();
         TPROBE_W(6);

@@ -1,9 +1,10 @@
 """Per-wave timeline of the Newsvendor K=30 rollout (nv_roll_kernel, 4 waves
-per 64-env workgroup; layout L1: two PTRS lane-pair waves, dynamics wave, obs
-wave with the multiplication-branch draws; L0 (NV_ROLL_LAYOUT=0): PTRS wave,
-multiplication wave, dynamics wave, obs wave).  Profiling only; needs the TIMING build (csrc `make timing`):
+per 64-env workgroup; layout L0: PTRS wave, multiplication wave, dynamics
+wave, obs wave; L1 names the roles of the lane-pair layout measured in
+commit b4c9eaf: two PTRS pair waves, dynamics, obs with the multiplication
+draws).  Profiling only; needs the TIMING build (csrc `make timing`):
 
-  INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so python tools/timing_nv_roll.py [L1|L0]
+  INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so python tools/timing_nv_roll.py [L0|L1]
 
 Probes (s_memrealtime, 100 MHz, lane 0 of every wave, row = workgroup * 4 +
 wave): 0 entry, 1 ready (stream: state + tables loaded; dynamics: barrier 0
@@ -38,7 +39,7 @@ def main():
     buf = np.zeros((8192, 8), dtype=np.uint64)
     rc = _capi.lib().invsim_debug_timing_nv(buf.ctypes.data_as(C.c_void_p), C.c_int64(buf.nbytes))
     assert rc == 0, rc
-    layout = sys.argv[1] if len(sys.argv) > 1 else "L1"   # L1: PTRS pairs + obs/mult wave; L0: the round-4 4-role kernel
+    layout = sys.argv[1] if len(sys.argv) > 1 else "L0"   # L0: the shipped 4-role kernel; L1: commit b4c9eaf's layout
     R = 4
     W = R * (n // 64)
     if layout == "L1":
