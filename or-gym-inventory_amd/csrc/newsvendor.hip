@@ -1109,10 +1109,10 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
 // trips per chunk).  As a fifth wave (commit 05546b1) the grid no longer fits
 // at once (<= 96 VGPRs, uneven placement of the fifth wave): 29.0 -> 20.4 G.
 // As two pair waves with the multiplication draws moved into the obs wave
-// (commit b4c9eaf) the obs wave became the tail: 29.3 -> 26.0 G.
-#ifndef NV_PTRS_PIPE
-#define NV_PTRS_PIPE 1   // the PTRS wave's trips software-pipelined (0: one candidate drawn and tested per trip)
-#endif
+// (commit b4c9eaf) the obs wave became the tail: 29.3 -> 26.0 G.  Software-
+// pipelining the PTRS wave's trips (the next candidate's uniforms drawn while
+// the pending one is tested, commit 3513fd2) measured no faster (28.9 against
+// 29.1-29.4 G): the trip is not bound by the generator's multiply chain.
 #define NV_ROLL_WAVES 4
 #define NV_ROLL_BOUNDS __launch_bounds__(4 * WAVE) __attribute__((amdgpu_waves_per_eu(4)))   // <= 128 VGPRs: the grid resident
 
@@ -1167,11 +1167,6 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
         PtrsConst c = nv_rate_const(P.par[4 * S + el]);
         bool mine = nv_mult_branch(c.lam) == multw;
         if (!multw) ts.flush(lane);
-        bool pend = false;          // NV_PTRS_PIPE: a PTRS candidate drawn ahead (uniforms pU, pV; state before them pg)
-        double pU = 0.0, pV = 0.0;
-        uint64_t pg_hi = 0, pg_lo = 0;
-        (void)pU;
-        (void)pV;
         bool reset_any = false;
         int t = t_start, cb = 0;
         int ci = 0;
@@ -1203,42 +1198,6 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
 #ifdef INVSIM_TIMING
                     uint32_t trips = 0;
 #endif
-#if NV_PTRS_PIPE
-                    // software-pipelined: each trip draws the NEXT candidate's two
-                    // uniforms while it tests the pending one.  A candidate always
-                    // consumes two uniforms, so where candidate n + 1 sits in the
-                    // stream does not depend on n's outcome; the candidate drawn
-                    // ahead stays pending across chunks of the episode and is
-                    // rewound (pg) before a reset's draws or the state store.
-                    if (!pend && nd > 0) {
-                        pg_hi = st.g.hi;
-                        pg_lo = st.g.lo;
-                        pU = st.g.next_double() - 0.5;
-                        pV = st.g.next_double();
-                        pend = true;
-                    }
-                    for (int j = 0; j < nd;) {
-#ifdef INVSIM_TIMING
-                        trips++;
-#endif
-                        const uint64_t nh = st.g.hi, nl = st.g.lo;    // before the next candidate
-                        const double Un = st.g.next_double() - 0.5;
-                        const double Vn = st.g.next_double();
-                        int64_t kd;
-                        const LgTab src{lg_l};
-                        const bool acc = ptrs_decide(
-                            c, pU, pV, [&](int64_t kk, bool &ok) { return src.fast(kk, c, ok); },
-                            [&](int64_t kk) { return src.exact(kk, c); }, kd);
-                        if (acc) {
-                            db[j * WAVE] = kd;
-                            j++;
-                        }
-                        pU = Un;
-                        pV = Vn;
-                        pg_hi = nh;
-                        pg_lo = nl;
-                    }
-#else
                     for (int j = 0; j < nd;) {
 #ifdef INVSIM_TIMING
                         trips++;
@@ -1267,7 +1226,6 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                             j++;
                         }
                     }
-#endif
 #ifdef INVSIM_TIMING
                     TTRIP_ADD(wave_max_u32(trips));
 #endif
@@ -1296,11 +1254,6 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             ci++;
 #endif
             if (rs && mine) {                      // reset() of the owner: 5 uniforms (:105-111)
-                if (pend) {                        // the candidate drawn ahead is not consumed
-                    st.g.hi = pg_hi;
-                    st.g.lo = pg_lo;
-                    pend = false;
-                }
                 nv_reset_regs<LT>(P, e, st, nullptr, false);
 #pragma unroll
                 for (int j = 0; j < 5; j++) pb[j * WAVE] = st.par[j];
@@ -1324,10 +1277,6 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             cb ^= 1;
         }
         nv_wg_sync();   // barrier nch: the obs wave's last chunk
-        if (pend) {         // the candidate drawn ahead is not consumed
-            st.g.hi = pg_hi;
-            st.g.lo = pg_lo;
-        }
         if (valid) {
             if (mine) P.cm.rng.store_state(e, st.g);
             if (reset_any && !multw) {
