@@ -358,18 +358,22 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
 def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
     """The step region as HIP-graph replays ("hipEvent around K
     launches (or a graph replay)"), reported beside the eager step line: one
-    replay = one episode cycle, periods + 1 invsim_step calls under NEXT_STEP
-    (each writing its row of a [C, N] output slab) and the episode fold of the
-    slab, recorded once with invsim.graphs.StepGraph.  ceil(steps / C) replays,
-    barrier + synchronize around them, max over ranks; one hipGraphLaunch per
-    cycle takes host submission out of the loop."""
+    replay = Q whole episode cycles (Q <= 4, at most the requested steps'
+    worth), Q * (periods + 1) invsim_step calls under NEXT_STEP (each writing
+    its row of a [Q C, N] output slab) and one episode fold of the slab -- the
+    eager region folds every 128 steps -- recorded once with
+    invsim.graphs.StepGraph.  ceil(steps / (Q C)) replays, barrier +
+    synchronize around them, max over ranks; one hipGraphLaunch per replay
+    takes host submission out of the loop."""
     import torch
     import invsim
     from invsim.distributed import EpisodeStats
     from invsim.graphs import StepGraph
     lib, h = env._lib, env._h
     N, O = env.num_envs, env.obs_dim
-    C = env._horizon() + 1
+    C1 = env._horizon() + 1
+    Q = max(1, min(4, 128 // C1, -(-steps // C1)))   # cycles per replay
+    C = Q * C1
     pool = max(1, args.pool)
     acts = make_actions(env, pool, 0, gen)
     rew = torch.empty((C, N), dtype=torch.float64, device=dev)
@@ -421,7 +425,8 @@ def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
     return {"value": total * N * world / el, "unit": "env-steps/s", "steps": total, "replays": reps,
             "steps_per_replay": C, "ms_per_step": el * 1e3 / total,
             "event_ms_per_step": e0.elapsed_time(e1) / total,
-            "what": "invsim_step x (periods+1) + episode fold per replay, one HIP graph (StepGraph)",
+            "cycles_per_replay": Q,
+            "what": "invsim_step x Q (periods+1) + one episode fold per replay, one HIP graph (StepGraph)",
             "episode_stats": dict(ep, source="the replays' own episode fold, one all-reduce after the region")}
 
 

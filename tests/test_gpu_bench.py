@@ -64,8 +64,9 @@ def test_bench_single_gpu_line():
     ep = d["episode_stats"]
     assert ep["episodes"] == 0 and ep["reward_sum"] != 0 and "no episode ends" in ep["note"]
     # the same step loop as graph replays: one 31-step cycle (+ fold) per replay
+    # (at most the requested steps' worth of cycles per replay)
     gr = d["graph"]
-    assert gr["steps"] == 31 and gr["replays"] == 1 and gr["value"] > 0
+    assert gr["steps"] == 31 and gr["replays"] == 1 and gr["cycles_per_replay"] == 1 and gr["value"] > 0
     assert gr["episode_stats"]["episodes"] == 65536
 
 

@@ -99,4 +99,4 @@ def test_bench_under_torchrun_nccl_one_rank():
     assert d["config"]["backend"] == "nccl" and d["ranks"] == 1 and d["n_gpus"] == 1
     assert d["episode_stats"]["episodes"] == 2 * 8192
     assert d["rollout"]["episode_stats"]["episodes"] == 30 * 8192
-    assert d["graph"]["episode_stats"]["episodes"] == 2 * 8192
+    assert d["graph"]["episode_stats"]["episodes"] == 2 * 8192 and d["graph"]["cycles_per_replay"] == 2
