@@ -632,6 +632,21 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla, i
             g.inc_lo = P.cm.rng.inc_lo[el];
             const double mu = P.par[4 * S + el];
             const bool mult_wg = brn;
+            // the chain's constants (nv_rate_const(mu), stored by its first launch),
+            // only the sampler branch's: the PTRS workgroup reads rows 0-4 for every
+            // lane, issued with the state and table loads instead of after mu has
+            // arrived (its lanes are ~95 % PTRS envs, so the rows' lines are read
+            // anyway); exp(-mu) only by the lanes that draw by multiplication
+            PtrsConst c;
+            c.lam = mu;
+            c.a = c.b = c.vr = c.loglam = c.log_invalpha = c.enlam = 0.0;
+            if (!mult_wg) {
+                c.a = P.pcon[el];
+                c.b = P.pcon[S + el];
+                c.vr = P.pcon[2 * S + el];
+                c.loglam = P.pcon[3 * S + el];
+                c.log_invalpha = P.pcon[4 * S + el];
+            }
             TableStage ts;
             if (!mult_wg) {
                 ts.dst = lg_l;
@@ -639,21 +654,7 @@ nv_step1_kernel(NvParams P, int sc, StepIO<float, float> io, int cur, int gla, i
                 ts.flush(lane);
             }
             const bool mine = mult_wg == (mu < 10 && mu != 0);
-            // the chain's constants (nv_rate_const(mu), stored by its first launch),
-            // read only by the lanes whose env this workgroup draws for, and only
-            // the sampler branch's: PTRS (mu >= 10) rows 0-4, else exp(-mu)
-            PtrsConst c;
-            c.lam = mu;
-            c.a = c.b = c.vr = c.loglam = c.log_invalpha = c.enlam = 0.0;
-            if (mine && mu >= 10) {
-                c.a = P.pcon[el];
-                c.b = P.pcon[S + el];
-                c.vr = P.pcon[2 * S + el];
-                c.loglam = P.pcon[3 * S + el];
-                c.log_invalpha = P.pcon[4 * S + el];
-            } else if (mine) {
-                c.enlam = P.pcon[5 * S + el];
-            }
+            if (mine && !(mu >= 10)) c.enlam = P.pcon[5 * S + el];
             c.a2 = 2 * c.a;
             c.k0 = 0;
             c.nk = 0;
