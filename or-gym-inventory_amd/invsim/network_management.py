@@ -19,7 +19,7 @@ import torch
 
 from . import _capi
 from .spaces import Box, batch_box
-from .topology import classify, compile_graph, default_graph, validate_inputs
+from .topology import check_market_receivers, classify, compile_graph, default_graph, validate_inputs
 from .vector import InvSimVectorEnv
 
 
@@ -92,6 +92,12 @@ class NetInvMgmtMasterEnv(InvSimVectorEnv):
 
     def _horizon(self):
         return self.num_periods
+
+    def reset(self, *, seed=None, options=None):
+        # :301-306 -> :240-267: the reference re-binds the market samplers at every
+        # reset; a lambda market must name this env (topology.check_market_receivers)
+        check_market_receivers(self.graph, self.retail_links, self)
+        return super().reset(seed=seed, options=options)
 
     def sample_action(self):
         hi = float(self.single_action_space.high[0]) if len(self.reorder_links) else 0.0

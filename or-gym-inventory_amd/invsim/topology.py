@@ -79,10 +79,13 @@ ZERO_DEMAND = (1, 0.0, 0, 0, 0.0)
 _SKIP_OPS = {"RESUME", "COPY_FREE_VARS", "CACHE", "NOP", "PUSH_NULL", "PRECALL", "MAKE_CELL"}
 
 
-def _lambda_method(f):
-    """The Generator method of ``lambda **p: <receiver>.np_random.<method>(**p)``
-    (network_management.py:125), read from the bytecode; None for any other shape
-    (arithmetic on the draw, another generator, positional arguments, ...)."""
+def _lambda_parts(f):
+    """(method, receiver opcode, receiver name) of
+    ``lambda **p: <receiver>.np_random.<method>(**p)`` (network_management.py:125),
+    read from the bytecode; None for any other shape (arithmetic on the draw,
+    another generator, positional arguments, ...).  The receiver is a free
+    variable (LOAD_DEREF) or a module global (LOAD_GLOBAL): the two ways a
+    lambda written outside the env can name it."""
     import dis
     import inspect
     code = getattr(f, "__code__", None)
@@ -95,7 +98,7 @@ def _lambda_method(f):
     if len(ins) < 5:
         return None
     recv, attr, meth = ins[:3]
-    if recv.opname not in ("LOAD_DEREF", "LOAD_GLOBAL", "LOAD_FAST", "LOAD_NAME") or recv.argval == kw:
+    if recv.opname not in ("LOAD_DEREF", "LOAD_GLOBAL"):
         return None
     if attr.opname != "LOAD_ATTR" or attr.argval != "np_random":
         return None
@@ -112,29 +115,108 @@ def _lambda_method(f):
             return None
     if calls != 1 or kwloads != 1 or ins[-1].opname != "RETURN_VALUE" or ins[-2].opname != "CALL_FUNCTION_EX":
         return None
-    return meth.argval
+    return meth.argval, recv.opname, recv.argval
 
 
 def sampler_method(f):
     """Name of the numpy Generator method a market's ``demand_dist_func`` calls.
 
-    Accepted: a method name (``"poisson"``, the package's own graphs), a bound
-    method of a numpy Generator (``env.np_random.poisson``), or the reference's
-    lambda shape ``lambda **p: self.np_random.poisson(**p)``
-    (network_management.py:125).  The device draws from the env's own stream,
-    as the reference's lambda over ``self.np_random`` does.  Anything else
-    raises: the device cannot run an arbitrary Python callable."""
+    Accepted: a method name (``"poisson"``, the package's own graphs) or the
+    reference's lambda shape ``lambda **p: <recv>.np_random.poisson(**p)``
+    (network_management.py:125).  The reference calls the lambda as written
+    (:263), so it draws from ``<recv>``'s generator: the device can only
+    reproduce that when ``<recv>`` is the env itself, which
+    ``check_market_receivers`` verifies at every ``reset()`` (the name may be
+    bound after the graph is built).  A Generator's bound method
+    (``rng.poisson``) is refused: its generator is a host object that is never
+    the env's own stream.  Anything else raises: the device cannot run an
+    arbitrary Python callable."""
     if isinstance(f, str):
         name = f
     elif getattr(f, "__self__", None) is not None and type(f.__self__).__name__ == "Generator":
-        name = getattr(f, "__name__", None)
+        raise ValueError(f"unsupported demand_dist_func {f!r}: a bound method of a host numpy Generator "
+                         f"draws from that generator (network_management.py:263), which the device "
+                         f"cannot; name the method ('poisson') or use "
+                         f"`lambda **p: <env>.np_random.<method>(**p)` over the env itself")
     else:
-        name = _lambda_method(f)
+        parts = _lambda_parts(f)
+        name = parts[0] if parts else None
     if name not in MARKET_SAMPLERS:
         raise ValueError(f"unsupported demand_dist_func {f!r}: it must be one of "
-                         f"{sorted(MARKET_SAMPLERS)} by name, a numpy Generator's bound method, or "
-                         f"`lambda **p: <env>.np_random.<method>(**p)`")
+                         f"{sorted(MARKET_SAMPLERS)} by name, or "
+                         f"`lambda **p: <env>.np_random.<method>(**p)` over the env itself")
     return name
+
+
+_UNBOUND = object()
+
+
+def lambda_receiver(f):
+    """The object a reference-shape market lambda names as ``<recv>`` in
+    ``<recv>.np_random.<method>(**p)``, resolved now, as the reference resolves
+    it when it calls the lambda (network_management.py:263); None for a method
+    name; ``_UNBOUND`` for a free variable or global with no value yet (or
+    None, on which the reference's call raises AttributeError)."""
+    if isinstance(f, str):
+        return None
+    parts = _lambda_parts(f)
+    if parts is None:
+        raise ValueError(f"unsupported demand_dist_func {f!r}")
+    _, op, name = parts
+    recv = _UNBOUND
+    if op == "LOAD_DEREF":
+        code = f.__code__
+        if name in code.co_freevars and f.__closure__ is not None:
+            try:
+                recv = f.__closure__[code.co_freevars.index(name)].cell_contents
+            except ValueError:                # empty cell
+                pass
+    else:
+        import builtins
+        g = getattr(f, "__globals__", {})
+        recv = g[name] if name in g else getattr(builtins, name, _UNBOUND)
+    return _UNBOUND if recv is None else recv   # None.np_random: the reference raises
+
+
+def is_env_receiver(recv, env):
+    """True when ``recv`` is ``env`` or a view over it (``invsim.compat``'s
+    single-env views keep the vector env as ``_v``; a wrapper may expose it as
+    ``unwrapped``)."""
+    if recv is env:
+        return True
+    for attr in ("_v", "unwrapped"):
+        try:
+            if recv is not None and object.__getattribute__(recv, attr) is env:
+                return True
+        except AttributeError:
+            pass
+    return False
+
+
+def check_market_receivers(g, retail_links, env):
+    """network_management.py:257-263: a market whose demand_dist_func is the
+    reference's lambda draws from ``<recv>.np_random``.  The device draws every
+    market from the env's own per-env stream, so ``<recv>`` must resolve to the
+    env: anything else (another object's generator, a name still unbound)
+    raises ValueError instead of silently drawing from the wrong stream.
+    Markets whose demand is user_D or zero never call the lambda and are not
+    checked (:250-255, :264-267)."""
+    tabs = env.topology.tables
+    for r, e in enumerate(retail_links):
+        attrs = g.edges[e]
+        if tabs["rl_user"][r] or "demand_dist_func" not in attrs or "dist_param" not in attrs:
+            continue
+        recv = lambda_receiver(attrs["demand_dist_func"])
+        if recv is None:
+            continue
+        if recv is _UNBOUND:
+            raise ValueError(f"market link {e}: the demand_dist_func lambda's receiver is not bound at "
+                             f"reset(); bind it to the env before resetting")
+        if not is_env_receiver(recv, env):
+            raise ValueError(f"market link {e}: demand_dist_func draws from {type(recv).__name__} "
+                             f"object's np_random, not this env's; the reference would call that "
+                             f"generator (network_management.py:263), the device can only draw from the "
+                             f"env's own stream -- bind the lambda to the env")
 
 
 def market_sampler(attrs):

@@ -1303,9 +1303,10 @@ def test_net_zero_demand_markets_vs_oracle(gpu, oracle, monkeypatch, generic):
     from test_topology import _three_market_graph
     if generic:
         monkeypatch.setenv("INVSIM_NET_GENERIC", "1")
-    g = _three_market_graph()
+    g, bind = _three_market_graph()
     n = 3000
     env = NetInvMgmtBacklogEnv(n, device=gpu, graph=g, record_demand=True)
+    bind(env)                                   # the lambda's receiver is the env (:125)
     assert env.kernel_variant == (0 if generic else 2)
     orc = oracle.OracleNet(n, graph=g)
     orc.seed(range(77, 77 + n))
@@ -1333,3 +1334,33 @@ def test_net_zero_demand_markets_vs_oracle(gpu, oracle, monkeypatch, generic):
         _assert_reward(r2[k].cpu().numpy(), e_rew, f"rollout step {k}")
     rng_gpu = env.state_fields()["rng"].cpu().numpy().view(np.uint64).T
     assert np.array_equal(rng_gpu, orc.rng_state())
+
+
+def test_net_lambda_receiver_is_checked_at_reset(gpu):
+    """VERDICT r04 item 1 (network_management.py:257-263, :125): a market lambda
+    draws from its receiver's generator in the reference; the device only
+    draws from the env's own stream, so reset() refuses a receiver that is not
+    the env (or the compat view over it) instead of drawing other demands."""
+    from invsim import NetInvMgmtBacklogEnv, compat
+    from test_topology import _three_market_graph
+
+    class Holder:
+        np_random = np.random.default_rng(0)
+    g, bind = _three_market_graph()
+    env = NetInvMgmtBacklogEnv(64, device=gpu, graph=g)
+    with pytest.raises(ValueError, match="not bound at reset"):
+        env.reset(seed=0)
+    bind(Holder())
+    with pytest.raises(ValueError, match="Holder object's np_random"):
+        env.reset(seed=0)
+    bind(env)
+    obs, _ = env.reset(seed=0)
+    assert obs.shape == (64, env.obs_dim)
+    view = compat.make("NetInvMgmtBacklogEnv", device=gpu, graph=g)
+    with pytest.raises(ValueError, match="not this env's"):
+        view.reset(seed=0)                  # bound to the other env
+    bind(view)
+    view.reset(seed=0)
+    view.step(np.full(view.action_space.shape, 5.0, np.float32))
+    env.close()
+    view.close()

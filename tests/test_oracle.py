@@ -260,15 +260,14 @@ def test_oracle_net_market_samplers_vs_numpy(oracle, fn, dp):
     through max(0, int(round(.)))."""
     from invsim.topology import custom_graph
     g = custom_graph()
-
-    class Env:
-        np_random = None
-    self = Env()
+    orc = None
     for e in list(g.edges()):
         if "L" not in g.edges[e]:
             g.edges[e]["dist_param"] = dict(dp)
-            # the reference's lambda shape for poisson (:125), a method name otherwise
-            g.edges[e]["demand_dist_func"] = (lambda **p: self.np_random.poisson(**p)) if fn == "poisson" else fn
+            # the reference's lambda shape for poisson (:125), over the env itself
+            # (bound below: the oracle env plays the reference's `self`), a method
+            # name otherwise
+            g.edges[e]["demand_dist_func"] = (lambda **p: orc.np_random.poisson(**p)) if fn == "poisson" else fn
     n, T = 16, 12
     orc = oracle.OracleNet(n, graph=g, num_periods=T)
     orc.seed(range(100, 100 + n))

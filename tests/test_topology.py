@@ -78,8 +78,11 @@ def test_market_sampler_sources():
                            "dist_param": {"lam": 3}})[:2] == (1, 3.0)
     assert market_sampler({"demand_dist_func": lambda **p: env.np_random.binomial(**p),
                            "dist_param": {"n": 5, "p": 0.5}}) == (2, 0.0, 5, 0, 0.5)
-    assert market_sampler({"demand_dist_func": env.np_random.integers,
+    assert market_sampler({"demand_dist_func": lambda **p: env.np_random.integers(**p),
                            "dist_param": {"low": 4, "high": 9}}) == (3, 0.0, 4, 9, 0.0)
+    # a host Generator's bound method draws from that generator, never the env's stream
+    with pytest.raises(ValueError, match="bound method of a host numpy Generator"):
+        market_sampler({"demand_dist_func": env.np_random.integers, "dist_param": {"low": 4, "high": 9}})
     assert market_sampler({"demand_dist_func": "integers", "dist_param": {"low": 9}}) == (3, 0.0, 0, 9, 0.0)
     assert market_sampler({"demand_dist_func": "geometric", "dist_param": {"p": 0.25}}) == (4, 0.0, 0, 0, 0.25)
     assert market_sampler({"demand_dist_func": "poisson", "dist_param": {}}) == (1, 1.0, 0, 0, 0.0)
@@ -131,18 +134,96 @@ def test_lambda_shapes_outside_the_reference_form_are_refused():
 
 def _three_market_graph():
     """The custom graph with one source-less market, one dist_param-only market
-    and one reference-style lambda market."""
+    and one reference-style lambda market, whose receiver is a free variable
+    that `bind(env)` sets to the env (network_management.py:125 names the env
+    itself; check_market_receivers refuses any other receiver at reset)."""
     from invsim.topology import custom_graph
+    env = None
 
-    class Env:
-        np_random = np.random.default_rng(0)
-    self = Env()
+    def bind(e):
+        nonlocal env
+        env = e
     g = custom_graph()
     a, b, c = [e for e in g.edges() if "L" not in g.edges[e]]
     del g.edges[a]["dist_param"], g.edges[a]["demand_dist_func"]
     del g.edges[b]["demand_dist_func"]
-    g.edges[c]["demand_dist_func"] = lambda **p: self.np_random.poisson(**p)
-    return g
+    g.edges[c]["demand_dist_func"] = lambda **p: env.np_random.poisson(**p)
+    return g, bind
+
+
+_GLOBAL_RECV = None
+
+
+def test_market_lambda_receiver_must_be_the_env():
+    """VERDICT r04 item 1 (network_management.py:257-263, :125): the reference
+    calls the market lambda as written, so `<recv>.np_random.<m>(**p)` draws
+    from <recv>'s generator.  The device draws from the env's own stream, so a
+    receiver that is not the env (or a view over it) raises at reset instead of
+    silently drawing different demands; the receiver is resolved at reset, as a
+    late-bound global or closure only binds after the graph is built."""
+    global _GLOBAL_RECV
+    from invsim.topology import check_market_receivers, compile_graph, custom_graph
+
+    class FakeEnv:                      # stands in for the vector env (no GPU here)
+        pass
+
+    class Holder:                       # some other object with a generator
+        np_random = np.random.default_rng(0)
+
+    class View:                         # invsim.compat's single-env view keeps the env as _v
+        def __init__(self, v):
+            self._v = v
+
+    def graph_with(f):
+        g = custom_graph()
+        c = [e for e in g.edges() if "L" not in g.edges[e]][2]
+        g.edges[c]["demand_dist_func"] = f
+        return g
+
+    def check(g):
+        env = FakeEnv()
+        env.topology = compile_graph(g, 30)
+        return env, (lambda: check_market_receivers(g, env.topology.retail_links, env))
+
+    # closure receiver bound to the env after construction: accepted
+    g, bind = _three_market_graph()
+    env, run = check(g)
+    with pytest.raises(ValueError, match="not bound at reset"):
+        run()
+    bind(env)
+    run()
+    bind(View(env))                     # the compat view over the env
+    run()
+    for foreign in (Holder(), View(FakeEnv()), FakeEnv()):
+        bind(foreign)
+        with pytest.raises(ValueError, match="not this env's"):
+            run()
+    bind(None)
+    with pytest.raises(ValueError, match="not bound at reset"):
+        run()
+    # a module-global receiver, resolved at check time, not at compile time
+    g = graph_with(lambda **p: _GLOBAL_RECV.np_random.poisson(**p))
+    env, run = check(g)
+    _GLOBAL_RECV = Holder()
+    with pytest.raises(ValueError, match="Holder object's np_random"):
+        run()
+    _GLOBAL_RECV = env
+    run()
+    _GLOBAL_RECV = None
+    with pytest.raises(ValueError, match="not bound at reset"):
+        run()
+    # numpy's global RandomState and a default_rng holder's bound method never compile
+    with pytest.raises(ValueError, match="unsupported demand_dist_func"):
+        compile_graph(graph_with(lambda **p: np.random.poisson(**p)), 30)
+    with pytest.raises(ValueError, match="bound method of a host numpy Generator"):
+        compile_graph(graph_with(np.random.default_rng(1).poisson), 30)
+    # a market replaying user_D never calls its lambda: not checked (:250-255)
+    h = Holder()
+    g = graph_with(lambda **p: h.np_random.poisson(**p))
+    c = [e for e in g.edges() if "L" not in g.edges[e]][2]
+    env = FakeEnv()
+    env.topology = compile_graph(g, 30, user_D={c: np.arange(30.0)})
+    check_market_receivers(g, env.topology.retail_links, env)
 
 
 def test_source_less_and_dist_param_only_markets_draw_nothing(oracle):
@@ -151,7 +232,7 @@ def test_source_less_and_dist_param_only_markets_draw_nothing(oracle):
     dist_param, and Poisson(lam) to the lambda market; user_D with sum 0 or
     sample_path=True falls through to the same rule."""
     from invsim.topology import compile_graph
-    g = _three_market_graph()
+    g, _ = _three_market_graph()
     t = compile_graph(g, 30).tables
     assert t["rl_dist"].tolist() == [1, 1, 1]
     assert t["rl_lam"].tolist() == [0.0, 0.0, 20.0]
