@@ -219,9 +219,10 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     # measured), so blocks are long
     LPB = 4                                         # launches per block (rollout / policy)
     R = LPB * K if K else 128
-    # two output slabs: the fold of one runs on a side stream while the steps
-    # write the other (events order slab reuse), so the reduction overlaps the
-    # env kernels instead of sitting between them
+    # two output slabs, alternating per block.  --fold inline (the default) runs
+    # each block's fold on the kernel stream after the block; --fold side runs it
+    # on a side stream while the steps write the other slab (events order slab
+    # reuse), measured slower because the fold then shares the CUs with the steps
     rew = torch.empty((2, R, N), dtype=torch.float64, device=dev)
     term = torch.empty((2, R, N), dtype=torch.bool, device=dev)
     trunc = torch.empty((2, R, N), dtype=torch.bool, device=dev)
@@ -322,8 +323,11 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     t0 = time.perf_counter()
     region(calls, True)
     if args.stop == "event":
-        # every timed launch and fold is on `stream`: its last event completing
-        # is the end of the work (hipEventSynchronize, no device-wide drain)
+        # the end of the work is `stream`'s last event completing
+        # (hipEventSynchronize, no device-wide drain); with --fold side the last
+        # block's fold runs on fstream, so `stream` waits for it first
+        if args.fold == "side":
+            stream.wait_stream(fstream)
         end_ev.record(stream)
         end_ev.synchronize()
         t1 = time.perf_counter()

@@ -197,8 +197,40 @@ int common_fields(invsim_handle *h, Layout &lay, int64_t &o_rng, int64_t &o_peri
     return 0;
 }
 
+// The A/B launch switches (kernels.hpp Knobs), read from the environment once,
+// here, when a handle is created: the only environment reads of the library.
+bool env_flag(const char *name, bool dflt) {
+    const char *v = std::getenv(name);
+    if (!v || !v[0]) return dflt;
+    return v[0] != '0';
+}
+
+Knobs read_knobs() {
+    Knobs k;
+    k.im_split = env_flag("INVSIM_IM_SPLIT", k.im_split);
+    k.im_la_last = env_flag("INVSIM_IM_LA_LAST", k.im_la_last);
+    k.im_roll = env_flag("INVSIM_IM_ROLL", k.im_roll);
+    k.im_pol_roll = env_flag("INVSIM_IM_POL_ROLL", k.im_pol_roll);
+    k.im_ahead = env_flag("INVSIM_IM_AHEAD", k.im_ahead);
+    if (const char *v = std::getenv("INVSIM_IM_ROLL3O_G2"); v && (v[0] == '0' || v[0] == '1'))
+        k.im_roll3o_g2 = (int8_t)(v[0] - '0');
+    if (const char *v = std::getenv("INVSIM_IM_ROLL3O_MAX_N"); v && v[0]) k.im_roll3o_max_n = (int64_t)atoll(v);
+    k.nv_xcd = env_flag("INVSIM_NV_XCD", k.nv_xcd);
+    k.nv_roll = env_flag("INVSIM_NV_ROLL", k.nv_roll);
+    k.nv_pol_roll = env_flag("INVSIM_NV_POL_ROLL", k.nv_pol_roll);
+    k.nv_ahead = env_flag("INVSIM_NV_AHEAD", k.nv_ahead);
+    k.net_roll = env_flag("INVSIM_NET_ROLL", k.net_roll);
+    k.net_roll3 = env_flag("INVSIM_NET_ROLL3", k.net_roll3);
+    k.net_split = env_flag("INVSIM_NET_SPLIT", k.net_split);
+    k.net_pol_roll = env_flag("INVSIM_NET_POL_ROLL", k.net_pol_roll);
+    k.net_ahead = env_flag("INVSIM_NET_AHEAD", k.net_ahead);
+    k.net_generic = env_flag("INVSIM_NET_GENERIC", k.net_generic);
+    return k;
+}
+
 void bind_common(invsim_handle *h, int64_t o_rng, int64_t o_period, int64_t o_status, int32_t ar) {
     Common &c = h->cm;
+    c.kn = read_knobs();
     c.N = h->N;
     c.Npad = h->Npad;
     c.autoreset = ar;
@@ -691,8 +723,7 @@ int invsim_create_netinvmgmt(const invsim_netinvmgmt_spec *s, int64_t n, int32_t
         rc = init_period(h, s->num_periods);
         // the reference's own graphs run the compile-time specialised kernel
         // (INVSIM_NET_GENERIC=1 forces the generic one, for cross-checks)
-        const char *gen = std::getenv("INVSIM_NET_GENERIC");
-        h->net_spec = (gen && gen[0] == '1') ? NET_SPEC_NONE : net_spec_match(*s);
+        h->net_spec = h->cm.kn.net_generic ? NET_SPEC_NONE : net_spec_match(*s);
         p.ahead = nullptr;
         if (rc == INVSIM_OK && h->net_spec != NET_SPEC_NONE) {   // lookahead cache: 2 slots x (2 + RL) rows
             hipError_t e = hipMalloc(&h->scratch, (size_t)(2 * (2 + p.RL) * h->Npad * sizeof(uint64_t)));

@@ -1340,11 +1340,14 @@ struct ImLt3o : ImLt3<L0, L1, L2> {
     static constexpr int RD = IM_ROLL3O_RD;                              // demand ring depth (chunks)
     static constexpr int M1 = 3, O = ImLt3<L0, L1, L2>::O;
     // tile, RHS table, demand ring, ibuf [2][CH][M1][WAVE] (inventory, dynamics ->
-    // obs wave), abuf [2][CH][M1][WAVE] (requested orders, dynamics -> obs wave),
-    // act_l [2][CH][2 M1][WAVE] u32 (actions, demand -> dynamics wave), alpha**t
-    static constexpr size_t lds(bool = false) {
-        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + 4 * CH * M1 * WAVE * 8 +
-               (size_t)2 * CH * 2 * M1 * WAVE * 4 + IM_AP_LDS * 8;
+    // obs wave), abuf [2][CH][M1][WAVE] (requested orders, dynamics -> obs wave;
+    // only with POL or staging), act_l [2][CH][2 M1][WAVE] u32 (actions, demand ->
+    // dynamics wave; only when staging open-loop actions), alpha**t
+    static constexpr size_t abuf_n(bool pol) { return (pol || IM_ROLL3O_STAGE) ? (size_t)2 * CH * M1 * WAVE : 0; }
+    static constexpr size_t actl_n(bool pol) { return (IM_ROLL3O_STAGE && !pol) ? (size_t)2 * CH * 2 * M1 * WAVE : 0; }
+    static constexpr size_t lds(bool pol) {
+        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + (size_t)2 * CH * M1 * WAVE * 8 +
+               abuf_n(pol) * 8 + actl_n(pol) * 4 + IM_AP_LDS * 8;
     }
 };
 
@@ -1371,9 +1374,9 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
     double *rhs_l = reinterpret_cast<double *>(im_tile + WAVE * O);
     int64_t *dbuf = reinterpret_cast<int64_t *>(rhs_l + RHS_LDS_MAX);   // [RD * CH][WAVE]
     int64_t *ibuf = dbuf + G::RD * CH * WAVE;                             // [2][CH][M1][WAVE]
-    int64_t *abuf = ibuf + 2 * CH * M1 * WAVE;                            // [2][CH][M1][WAVE]
-    uint32_t *act_l = reinterpret_cast<uint32_t *>(abuf + 2 * CH * M1 * WAVE);   // [2][CH][2 M1][WAVE]
-    double *ap_l = reinterpret_cast<double *>(act_l + 2 * CH * 2 * M1 * WAVE);   // alpha**t, t < periods
+    int64_t *abuf = ibuf + 2 * CH * M1 * WAVE;                            // [2][CH][M1][WAVE] (POL / staged)
+    uint32_t *act_l = reinterpret_cast<uint32_t *>(abuf + G::abuf_n(POL));  // [2][CH][2 M1][WAVE] (staged)
+    double *ap_l = reinterpret_cast<double *>(act_l + G::actl_n(POL));      // alpha**t, t < periods
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t N = P.cm.N;
     const int64_t S = P.cm.Npad;
@@ -1722,67 +1725,20 @@ __global__ void __launch_bounds__(256) im_commit_kernel(ImParams P, int slot) {
 
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
-// INVSIM_IM_SPLIT=0 keeps single steps on the one-wave kernel (A/B measurements)
-inline bool im_split_enabled() {
-    const char *s = getenv("INVSIM_IM_SPLIT");
-    return !(s && s[0] == '0');
-}
-
-// INVSIM_IM_LA_LAST=1 puts the lookahead workgroups at the end of the grid (A/B)
-inline bool im_la_last() {
-    const char *s = getenv("INVSIM_IM_LA_LAST");
-    return s && s[0] == '1';
-}
-
-// INVSIM_IM_ROLL=0 keeps rollouts on the one-wave kernel (A/B measurements, tests)
-// largest batch for the 3-role rollout (INVSIM_IM_ROLL3O_MAX_N overrides: A/B, tests)
-inline int64_t im_roll3o_max_n() {
-    const char *v = getenv("INVSIM_IM_ROLL3O_MAX_N");
-    return v ? (int64_t)atoll(v) : 32768;
-}
-
-// Two 64-env groups per 6-wave workgroup: the default for policy rollouts
-// (BaseStock at 32 768 envs: 63.1-64.8 against 66.5-67.7 us per 30 steps),
-// equal open loop (profiles/r03/launch/g2_stage.txt).  INVSIM_IM_ROLL3O_G2=1 /
-// =0 forces it on / off for both (A/B, tests).
-inline bool im_roll3o_g2(bool pol) {
-    const char *v = getenv("INVSIM_IM_ROLL3O_G2");
-    if (v && v[0] == '1') return true;
-    if (v && v[0] == '0') return false;
-    return pol;
-}
-
-inline bool im_roll_enabled() {
-    const char *s = getenv("INVSIM_IM_ROLL");
-    return !(s && s[0] == '0');
-}
-
-// INVSIM_IM_POL_ROLL=0 keeps policy rollouts on im_run_kernel (A/B, tests)
-inline bool im_pol_roll_enabled() {
-    const char *s = getenv("INVSIM_IM_POL_ROLL");
-    return !(s && s[0] == '0');
-}
-
-// INVSIM_IM_AHEAD=0 turns the demand lookahead off (A/B measurements)
-inline bool im_ahead_enabled() {
-    const char *s = getenv("INVSIM_IM_AHEAD");
-    return !(s && s[0] == '0');
-}
-
 // the lock-step split step kernel applies (both streams)
 inline bool im_split_applies(const ImParams &p, int t_u, const PolicyIO *pol, const StepIO<int64_t, int64_t> &io) {
     return !pol && io.K == 1 && t_u >= 0 && t_u < p.periods && io.obs &&
-           !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.periods) && im_split_enabled();
+           !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.periods) && p.cm.kn.im_split;
 }
 
 // the 2-/3-role rollout kernels of the reference's default lead times apply
 // (open loop, or the in-kernel BaseStock / ConstantOrder agents)
 inline bool im_roll_applies(const ImParams &p, int M1, int t_u, const PolicyIO *pol,
                             const StepIO<int64_t, int64_t> &io) {
-    const bool pol_roll = pol && (pol->kind == POL_BASE_STOCK || pol->kind == POL_CONSTANT) && im_pol_roll_enabled();
+    const bool pol_roll = pol && (pol->kind == POL_BASE_STOCK || pol->kind == POL_CONSTANT) && p.cm.kn.im_pol_roll;
     return (!pol || pol_roll) && io.K > 1 && t_u >= 0 && p.cm.autoreset != AR_SAME_STEP && p.dist == 1 &&
            !p.cm.info_rec && M1 == 3 && p.L[0] == 1 && p.L[1] == 5 && p.L[2] == 10 && p.lt_max == 10 &&
-           im_roll_enabled();
+           p.cm.kn.im_roll;
 }
 
 template <class RG>
@@ -1797,9 +1753,13 @@ hipError_t im_roll_launch(const ImParams &p, bool backlog, int t_u, const Policy
     // wave's chain is the step time, so split it (measured on MI355X:
     // LostSales 32768 envs 87.5 -> 77.7 us per K = 30; at 65536 the
     // 2-role kernel is faster, 118 vs 152 us)
-    const bool three = p.cm.N <= im_roll3o_max_n() && p.periods <= IM_AP_LDS;   // alpha**t table in LDS
+    const bool three = p.cm.N <= p.cm.kn.im_roll3o_max_n && p.periods <= IM_AP_LDS;   // alpha**t table in LDS
     // two groups per workgroup when the group count is even (every workgroup full)
-    const bool two = three && im_roll3o_g2(pol != nullptr) && (g3.x % 2) == 0;
+    // two 64-env groups per 6-wave workgroup: the default for policy rollouts
+    // (BaseStock at 32 768 envs: 63.1-64.8 against 66.5-67.7 us per 30 steps),
+    // equal open loop (profiles/r03/launch/g2_stage.txt)
+    const bool g2 = p.cm.kn.im_roll3o_g2 < 0 ? pol != nullptr : p.cm.kn.im_roll3o_g2 == 1;
+    const bool two = three && g2 && (g3.x % 2) == 0;
     const dim3 g6(g3.x / 2);
 #define R_(B, POL)                                                                                                    \
     do {                                                                                                              \
@@ -1847,12 +1807,12 @@ hipError_t im_run_launch_ph(const ImParams &p, int M1, bool backlog, int t_u, co
     if (im_split_applies(p, t_u, pol, io)) {   // the split step kernel, with the demand-only lookahead
         const size_t lds2 = lds + WAVE * sizeof(int64_t);
         ImParams q = p;
-        if (!im_ahead_enabled()) q.ahead = nullptr;
+        if (!p.cm.kn.im_ahead) q.ahead = nullptr;
         const bool hit = ahead && q.ahead;
         const int gla = hit ? (int)grid_for(p.cm.N, 2 * WAVE) : 0;
         const dim3 grid2(grid.x + gla), block2(2 * WAVE);
         const int cur = slot;
-        const int la0 = im_la_last() ? (int)grid.x : 0;
+        const int la0 = p.cm.kn.im_la_last ? (int)grid.x : 0;
 #define S_(M, B)                                                                                        \
     do {                                                                                                \
         if (npd) {                                                                                      \
@@ -1914,7 +1874,7 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
         const size_t lds2 = lds + WAVE * sizeof(int64_t);
         const dim3 block2(2 * WAVE);
         ImParams q = p;
-        if (!im_ahead_enabled()) q.ahead = nullptr;
+        if (!p.cm.kn.im_ahead) q.ahead = nullptr;
         if (ahead && !q.ahead) {      // lookahead switched off: commit, then draw inline
             const hipError_t ce = im_commit_launch(p, slot, s);
             ahead = false;
@@ -1924,7 +1884,7 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
         const int gla = hit ? (int)grid_for(p.cm.N, 2 * WAVE) : 0;   // lookahead workgroups
         const dim3 grid2(grid.x + gla);
         const int cur = slot;
-        const int la0 = im_la_last() ? (int)grid.x : 0;   // lookahead workgroups first (default) or last
+        const int la0 = p.cm.kn.im_la_last ? (int)grid.x : 0;   // lookahead workgroups first (default) or last
 #define S_(M, B)                                                                                        \
     do {                                                                                                \
         if (npd) {                                                                                      \

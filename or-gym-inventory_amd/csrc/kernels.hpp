@@ -92,6 +92,31 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #define TWAIT() do {} while (0)
 #endif
 
+// Launch-choice switches for A/B measurements and tests (INVSIM_* environment
+// variables).  capi.hip reads the environment ONCE, when a handle is created
+// (read_knobs), into Common::kn; the launchers read only these fields, so a
+// variable set after creation changes nothing.  Kernels ignore them.
+struct Knobs {
+    bool im_split = true;            // INVSIM_IM_SPLIT=0: single steps on the one-wave kernel
+    bool im_la_last = false;         // INVSIM_IM_LA_LAST=1: lookahead workgroups at the end of the grid
+    bool im_roll = true;             // INVSIM_IM_ROLL=0: rollouts on the one-wave kernel
+    bool im_pol_roll = true;         // INVSIM_IM_POL_ROLL=0: policy rollouts on im_run_kernel
+    bool im_ahead = true;            // INVSIM_IM_AHEAD=0: no demand lookahead
+    int8_t im_roll3o_g2 = -1;        // INVSIM_IM_ROLL3O_G2=1 / =0: two groups per workgroup on / off
+                                     //   (-1: policy rollouts only)
+    bool nv_xcd = true;              // INVSIM_NV_XCD=0: lookahead workgroups adjacent, not XCD-paired
+    bool nv_roll = true;             // INVSIM_NV_ROLL=0: rollouts on nv_run_kernel
+    bool nv_pol_roll = true;         // INVSIM_NV_POL_ROLL=0: policy rollouts on nv_run_kernel
+    bool nv_ahead = true;            // INVSIM_NV_AHEAD=0: no demand lookahead
+    bool net_roll = true;            // INVSIM_NET_ROLL=0: rollouts on net_spec_kernel
+    bool net_roll3 = true;           // INVSIM_NET_ROLL3=0: net_roll_kernel instead of net_roll3o_kernel
+    bool net_split = true;           // INVSIM_NET_SPLIT=0: the step on the one-wave net_step1_kernel
+    bool net_pol_roll = true;        // INVSIM_NET_POL_ROLL=0: ConstantOrder rollouts on net_spec_kernel
+    bool net_ahead = true;           // INVSIM_NET_AHEAD=0: no demand lookahead
+    bool net_generic = false;        // INVSIM_NET_GENERIC=1: the generic kernel for the built-in graphs
+    int64_t im_roll3o_max_n = 32768; // INVSIM_IM_ROLL3O_MAX_N: largest batch for the 3-role rollout
+};
+
 struct Common {
     int64_t N;       // envs in this handle
     int64_t Npad;    // SoA row stride (elements)
@@ -104,6 +129,7 @@ struct Common {
     void *info_rec;        // optional per-step info record (invsim_set_info_record), last step of a launch
     int32_t philox;        // demand stream: 0 numpy PCG64 (parity), 1 fast Philox (PhiloxGen)
     uint64_t ph_step;      // fast stream: the handle's launch-step counter at this launch's first step
+    Knobs kn;              // host-side launch choices (read at handle creation)
 };
 
 // ---------------------------------------------------------------- Newsvendor

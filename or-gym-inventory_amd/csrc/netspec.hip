@@ -1399,41 +1399,9 @@ int net_spec_match(const invsim_netinvmgmt_spec &h) {
     return NET_SPEC_NONE;
 }
 
-// INVSIM_NET_ROLL=0 keeps rollouts on net_spec_kernel (A/B measurements, tests)
-static bool net_roll_enabled() {
-    const char *v = getenv("INVSIM_NET_ROLL");
-    return !(v && v[0] == '0');
-}
-
-// Rollout kernel choice: the 3-role net_roll3o_kernel (measured on MI355X,
-// 30-step launches: 32 768 envs 69 vs 97 us, 65 536 envs 140 vs 185 us against
-// net_roll_kernel); INVSIM_NET_ROLL3=0 keeps net_roll_kernel (A/B, tests).
-static bool net_roll3_use(int64_t) {
-    const char *v = getenv("INVSIM_NET_ROLL3");
-    return !(v && v[0] == '0');
-}
-
 template <class G>
 static size_t spec_lds_bytes() {
     return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float) + (size_t)G::RL * RHS_LDS_MAX * sizeof(double);
-}
-
-// INVSIM_NET_SPLIT=0 keeps the step on the one-wave net_step1_kernel (A/B, tests)
-static bool net_split_enabled() {
-    const char *v = getenv("INVSIM_NET_SPLIT");
-    return !(v && v[0] == '0');
-}
-
-// INVSIM_NET_POL_ROLL=0 keeps ConstantOrder rollouts on net_spec_kernel (A/B, tests)
-static bool net_pol_roll_enabled() {
-    const char *v = getenv("INVSIM_NET_POL_ROLL");
-    return !(v && v[0] == '0');
-}
-
-// INVSIM_NET_AHEAD=0 turns the step's demand lookahead off (A/B measurements)
-static bool net_ahead_enabled() {
-    const char *v = getenv("INVSIM_NET_AHEAD");
-    return !(v && v[0] == '0');
 }
 
 template <class G>
@@ -1446,12 +1414,12 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
     // fast stream: the split step kernel with a demand-only lookahead, the
     // rollout kernels with counter-positioned draws, net_spec_kernel otherwise
     const bool ph = p.cm.philox != 0;
-    if (p.ahead && net_ahead_enabled() && !pol && io.K == 1 && t_u >= 0 && t_u < p.T && io.obs &&
+    if (p.ahead && p.cm.kn.net_ahead && !pol && io.K == 1 && t_u >= 0 && t_u < p.T && io.obs &&
         !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.T)) {
         const bool hit = ahead;
         const int gla = hit ? (int)((p.cm.N + WAVE - 1) / WAVE) : 0;
         const dim3 grid2(grid.x + gla);
-        if (net_split_enabled() || ph) {
+        if (p.cm.kn.net_split || ph) {
             const int gl2 = hit ? (int)((p.cm.N + 2 * WAVE - 1) / (2 * WAVE)) : 0;
             const dim3 g2(grid.x + gl2), b2(2 * WAVE);
             if (ph) {
@@ -1484,15 +1452,18 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
         else hipLaunchKernelGGL((net_spec_kernel<G, TU, ONE, POL, Pcg>), grid, block, lds, s, p, t_u, io, pv);         \
     } while (0)
     // ... and the in-kernel ConstantOrder agent on the 3-role kernel
-    const bool pol_roll = pol && pol->kind == POL_CONSTANT && net_pol_roll_enabled();
-    if ((!pol || pol_roll) && io.K > 1 && t_u >= 0 && !p.cm.info_rec && net_roll_enabled() &&
+    const bool pol_roll = pol && pol->kind == POL_CONSTANT && p.cm.kn.net_pol_roll;
+    if ((!pol || pol_roll) && io.K > 1 && t_u >= 0 && !p.cm.info_rec && p.cm.kn.net_roll &&
         (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
         const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE));
         using R3 = NetRoll3<G, NET_ROLL3_CH>;
+        // the 3-role net_roll3o_kernel by default (measured on MI355X, 30-step
+        // launches: 32 768 envs 69 vs 97 us, 65 536 envs 140 vs 185 us against
+        // net_roll_kernel)
 #define RK_(RG)                                                                                                       \
     do {                                                                                                              \
         if (pol) hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, true, RG>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv); \
-        else if (net_roll3_use(p.cm.N)) hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, false, RG>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv); \
+        else if (p.cm.kn.net_roll3) hipLaunchKernelGGL((net_roll3o_kernel<G, NET_ROLL3_CH, false, RG>), gr, dim3(3 * WAVE), R3::lds(), s, p, t_u, io, pv); \
         else hipLaunchKernelGGL((net_roll_kernel<G, RG>), gr, dim3(2 * WAVE), NetRoll<G>::lds(), s, p, t_u, io);    \
     } while (0)
         if (ph) RK_(PhiloxGen);

@@ -1473,19 +1473,6 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     TPROBE_W(6);
 }
 
-// INVSIM_NV_XCD=0 keeps the lookahead workgroups of a group adjacent instead of
-// on one XCD (A/B measurements)
-inline bool nv_xcd_pair_enabled() {
-    const char *v = getenv("INVSIM_NV_XCD");
-    return !(v && v[0] == '0');
-}
-
-// INVSIM_NV_ROLL=0 keeps rollouts on nv_run_kernel (A/B measurements, tests)
-inline bool nv_roll_enabled() {
-    const char *v = getenv("INVSIM_NV_ROLL");
-    return !(v && v[0] == '0');
-}
-
 // cm.rng <- the committed slot of the lookahead cache
 __global__ void __launch_bounds__(256) nv_commit_kernel(NvParams P, int slot) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1494,18 +1481,6 @@ __global__ void __launch_bounds__(256) nv_commit_kernel(NvParams P, int slot) {
     const uint64_t *A = P.ahead + (int64_t)slot * 3 * S;
     P.cm.rng.hi[e] = A[e];
     P.cm.rng.lo[e] = A[S + e];
-}
-
-// INVSIM_NV_POL_ROLL=0 keeps policy rollouts on nv_run_kernel (A/B measurements, tests)
-inline bool nv_pol_roll_enabled() {
-    const char *v = getenv("INVSIM_NV_POL_ROLL");
-    return !(v && v[0] == '0');
-}
-
-// INVSIM_NV_AHEAD=0 turns the demand lookahead off (A/B measurements)
-inline bool nv_ahead_enabled() {
-    const char *s = getenv("INVSIM_NV_AHEAD");
-    return !(s && s[0] == '0');
 }
 
 __global__ void __launch_bounds__(256)
@@ -1560,7 +1535,7 @@ hipError_t nv_launch_rg(const NvParams &p, int t_u, const PolicyIO *pol, const S
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
     PolicyIO none{};
     const PolicyIO &pv = pol ? *pol : none;
-    const bool la = p.ahead && nv_ahead_enabled();
+    const bool la = p.ahead && p.cm.kn.nv_ahead;
     if (la && !pol && io.K == 1 && t_u >= 0 && t_u < p.step_limit && io.obs &&
         !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.step_limit)) {
         const bool produce = t_u + 1 < p.step_limit;
@@ -1571,7 +1546,7 @@ hipError_t nv_launch_rg(const NvParams &p, int t_u, const PolicyIO *pol, const S
             const int gla = hit ? (produce ? 2 : (ph ? 0 : 1)) * (int)grid_for(p.cm.N, WAVE) : 0;
             const dim3 grid2(grid.x + gla);
             const int cur = slot;
-            const int xp = nv_xcd_pair_enabled() ? 1 : 0;
+            const int xp = p.cm.kn.nv_xcd ? 1 : 0;
 #define S_(X)                                                                                                \
     do {                                                                                                     \
         if (hit && produce) hipLaunchKernelGGL((nv_step1_kernel<X, true, true, RG>), grid2, block, lds, s, p, t_u, io, cur, gla, xp);  \
@@ -1594,8 +1569,8 @@ hipError_t nv_launch_rg(const NvParams &p, int t_u, const PolicyIO *pol, const S
         ahead = false;
         if (ce != hipSuccess) return ce;
     }
-    if ((!pol || nv_pol_roll_enabled()) && io.K > 1 && t_u >= 0 && p.L > 0 &&
-        p.cm.autoreset != AR_SAME_STEP && nv_roll_enabled()) {
+    if ((!pol || p.cm.kn.nv_pol_roll) && io.K > 1 && t_u >= 0 && p.L > 0 &&
+        p.cm.autoreset != AR_SAME_STEP && p.cm.kn.nv_roll) {
         const dim3 gr(grid_for(p.cm.N, WAVE)), br(NV_ROLL_WAVES * WAVE);
         bool done = true;
 #define R_(X)                                                                                              \

@@ -53,3 +53,18 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+def knob_envs(monkeypatch, var, values, make):
+    """One env per value of the INVSIM_* launch switch `var` (None: unset).
+    libinvsim reads the switches once, when a handle is created (kernels.hpp
+    Knobs), so each env is made with its value set and keeps it."""
+    envs = []
+    for v in values:
+        if v is None:
+            monkeypatch.delenv(var, raising=False)
+        else:
+            monkeypatch.setenv(var, v)
+        envs.append(make())
+    monkeypatch.delenv(var, raising=False)
+    return envs

@@ -121,3 +121,30 @@ def test_python_env_fails_loudly_without_gpu():
     from invsim import InvManagementBacklogEnv
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         InvManagementBacklogEnv(4)
+
+
+def test_launch_switches_are_read_only_at_handle_creation():
+    """the INVSIM_* A/B switches are read from the
+    environment once, when a handle is created (capi.hip read_knobs into
+    Common::kn), never on a launch path: `getenv` appears only in capi.hip's
+    env_flag / read_knobs, and every switch the launchers use is a Knobs
+    field."""
+    import re
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "or-gym-inventory_amd", "csrc")
+    hits = {}
+    for name in sorted(os.listdir(csrc)):
+        if name.endswith((".hip", ".hpp")):
+            src = open(os.path.join(csrc, name)).read()
+            for m in re.finditer(r"\bgetenv\s*\(", src):
+                hits.setdefault(name, []).append(src.count("\n", 0, m.start()) + 1)
+    assert list(hits) == ["capi.hip"], hits
+    capi = open(os.path.join(csrc, "capi.hip")).read()
+    a = capi.index("bool env_flag(")
+    b = capi.index("void bind_common(")
+    lines = [capi.count("\n", 0, i) + 1 for i in (a, b)]
+    assert all(lines[0] <= ln < lines[1] for ln in hits["capi.hip"]), (hits, lines)
+    assert "c.kn = read_knobs();" in capi[b:b + 200]
+    kern = open(os.path.join(csrc, "kernels.hpp")).read()
+    fields = set(re.findall(r"^\s+(?:bool|int8_t|int64_t) (\w+) = ", kern[kern.index("struct Knobs"):kern.index("struct Common")], re.M))
+    reads = set(re.findall(r'"INVSIM_(\w+)"', capi[a:b]))
+    assert {f.upper() for f in fields} == reads, (fields, reads)

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import IM_GOLDENS, NET_GOLDENS, NV_GOLDENS, im_kwargs, load_golden, nv_kwargs
+from conftest import IM_GOLDENS, NET_GOLDENS, NV_GOLDENS, im_kwargs, knob_envs, load_golden, nv_kwargs
 
 pytestmark = pytest.mark.gpu
 
@@ -568,8 +568,9 @@ def test_invmgmt_split_kernel_equals_one_wave(gpu, cfg, autoreset, monkeypatch):
     import invsim
     cls = getattr(invsim, cfg["cls"])
     n, K = 1000, 65                      # padded lanes; two episodes and the resets between them
-    envs = [cls(n, device=gpu, autoreset_mode=autoreset, record_demand=True, record_info=True, **cfg["kw"])
-            for _ in range(2)]
+    envs = knob_envs(monkeypatch, "INVSIM_IM_SPLIT", ("1", "0"),
+                     lambda: cls(n, device=gpu, autoreset_mode=autoreset, record_demand=True, record_info=True,
+                                 **cfg["kw"]))
     m1 = envs[0].action_dim
     g = torch.Generator(device=gpu).manual_seed(3)
     a = torch.randint(-5, 120, (K, n, m1), device=gpu, dtype=torch.int64, generator=g)
@@ -577,8 +578,7 @@ def test_invmgmt_split_kernel_equals_one_wave(gpu, cfg, autoreset, monkeypatch):
         env.reset(seed=77)
     for k in range(K):
         out = []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_IM_SPLIT", "1" if i == 0 else "0")
+        for env in envs:
             o, r, te, tr, info = env.step(a[k])
             out.append((o.clone(), r.clone(), te.clone(), tr.clone(),
                         {key: v.clone() for key, v in info.items() if torch.is_tensor(v)}))
@@ -590,7 +590,6 @@ def test_invmgmt_split_kernel_equals_one_wave(gpu, cfg, autoreset, monkeypatch):
                 assert torch.equal(out[0][4][key][msk], out[1][4][key][msk]), k
             else:
                 assert torch.equal(out[0][4][key], out[1][4][key]), (key, k)
-    monkeypatch.delenv("INVSIM_IM_SPLIT")
     assert torch.equal(envs[0].get_state(), envs[1].get_state())
 
 
@@ -605,15 +604,15 @@ def test_invmgmt_demand_lookahead_mixed_calls(gpu, kw, monkeypatch):
     import invsim
     from invsim.policies import BaseStockAgent
     n = 777
-    envs = [invsim.InvManagementBacklogEnv(n, device=gpu, periods=9, record_demand=True, **kw) for _ in range(2)]
+    envs = knob_envs(monkeypatch, "INVSIM_IM_AHEAD", ("1", "0"),
+                     lambda: invsim.InvManagementBacklogEnv(n, device=gpu, periods=9, record_demand=True, **kw))
     g = torch.Generator(device=gpu).manual_seed(5)
     A = torch.randint(-5, 150, (200, n, 3), device=gpu, dtype=torch.int64, generator=g)
     pos = [0]
 
     def both(fn):
         outs = []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_IM_AHEAD", "1" if i == 0 else "0")
+        for env in envs:
             outs.append(fn(env))
         return outs
 
@@ -667,15 +666,15 @@ def test_newsvendor_demand_lookahead_mixed_calls(gpu, kw, monkeypatch):
     import invsim
     from invsim.policies import OrderUpToHeuristicAgent
     n = 700
-    envs = [invsim.NewsvendorEnv(n, device=gpu, step_limit=7, record_demand=True, **kw) for _ in range(2)]
+    envs = knob_envs(monkeypatch, "INVSIM_NV_AHEAD", ("1", "0"),
+                     lambda: invsim.NewsvendorEnv(n, device=gpu, step_limit=7, record_demand=True, **kw))
     g = torch.Generator(device=gpu).manual_seed(6)
     A = torch.rand((100, n, 1), device=gpu, generator=g) * 400 - 20
     pos = [0]
 
     def both(fn):
         outs = []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_NV_AHEAD", "1" if i == 0 else "0")
+        for env in envs:
             outs.append(fn(env))
         return outs
 
@@ -745,11 +744,11 @@ def test_invmgmt_register_window_rollout_equals_one_wave(gpu, monkeypatch, cls, 
     (wide >= 2^32 orders included; ring slots of earlier episodes included,
     over horizons that are and are not multiples of the ring lengths)."""
     import invsim
-    envs = []
-    for i in range(2):
-        env = getattr(invsim, cls)(n, device=gpu, autoreset_mode=mode, record_demand=True, periods=periods)
+    envs = knob_envs(monkeypatch, "INVSIM_IM_ROLL", ("1", "0"),
+                     lambda: getattr(invsim, cls)(n, device=gpu, autoreset_mode=mode, record_demand=True,
+                                                  periods=periods))
+    for env in envs:
         env.reset(seed=41)
-        envs.append(env)
     g = torch.Generator(device=gpu)
     g.manual_seed(9)
     for k in range(pre):
@@ -760,15 +759,13 @@ def test_invmgmt_register_window_rollout_equals_one_wave(gpu, monkeypatch, cls, 
         a = torch.randint(-5, 260, (K, n, 3), device=gpu, dtype=torch.int64, generator=g)
         a[::2, ::97, 1] = (1 << 32) + 5         # wide requested orders (every other step): the int64 side ring
         outs, dems = [], []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_IM_ROLL", "1" if i == 0 else "0")
+        for env in envs:
             outs.append(env.rollout(a))
             dems.append(env._demand.clone())
         for x, y in zip(outs[0], outs[1]):
             assert torch.equal(x, y), K
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
-    monkeypatch.delenv("INVSIM_IM_ROLL")
 
 
 @pytest.mark.parametrize("graph,backlog,n,pre,Ks,mode", [
@@ -786,12 +783,11 @@ def test_net_demand_wave_rollout_equals_one_wave(gpu, monkeypatch, graph, backlo
     import invsim
     from invsim.topology import custom_graph, default_graph
     mk_g = default_graph if graph == "default" else custom_graph
-    envs = []
-    for i in range(2):
-        env = invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), backlog=backlog, autoreset_mode=mode,
-                                         record_demand=True)
+    envs = knob_envs(monkeypatch, "INVSIM_NET_ROLL", ("1", "0"),
+                     lambda: invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), backlog=backlog,
+                                                        autoreset_mode=mode, record_demand=True))
+    for env in envs:
         env.reset(seed=41)
-        envs.append(env)
     g = torch.Generator(device=gpu)
     g.manual_seed(9)
     A = envs[0].action_dim
@@ -802,15 +798,13 @@ def test_net_demand_wave_rollout_equals_one_wave(gpu, monkeypatch, graph, backlo
     for K in Ks:
         a = torch.rand((K, n, A), device=gpu, generator=g) * 260 - 5
         outs, dems = [], []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_NET_ROLL", "1" if i == 0 else "0")
+        for env in envs:
             outs.append(env.rollout(a))
             dems.append(env._demand.clone())
         for x, y in zip(outs[0], outs[1]):
             assert torch.equal(x, y), K
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
-    monkeypatch.delenv("INVSIM_NET_ROLL")
 
 
 @pytest.mark.parametrize("L,step_limit,n,pre,Ks,mode", [
@@ -827,12 +821,11 @@ def test_newsvendor_stream_wave_rollout_equals_one_wave(gpu, monkeypatch, L, ste
     INVSIM_NV_ROLL=0 keeps it on nv_run_kernel.  Same state in, identical
     outputs, demand record and state out."""
     import invsim
-    envs = []
-    for i in range(2):
-        env = invsim.NewsvendorEnv(n, device=gpu, lead_time=L, step_limit=step_limit, autoreset_mode=mode,
-                                   record_demand=True)
+    envs = knob_envs(monkeypatch, "INVSIM_NV_ROLL", ("1", "0"),
+                     lambda: invsim.NewsvendorEnv(n, device=gpu, lead_time=L, step_limit=step_limit,
+                                                  autoreset_mode=mode, record_demand=True))
+    for env in envs:
         env.reset(seed=41)
-        envs.append(env)
     g = torch.Generator(device=gpu)
     g.manual_seed(9)
     for k in range(pre):
@@ -842,15 +835,13 @@ def test_newsvendor_stream_wave_rollout_equals_one_wave(gpu, monkeypatch, L, ste
     for K in Ks:
         a = torch.rand((K, n, 1), device=gpu, generator=g) * 2600 - 100
         outs, dems = [], []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_NV_ROLL", "1" if i == 0 else "0")
+        for env in envs:
             outs.append(env.rollout(a))
             dems.append(env._demand.clone())
         for x, y in zip(outs[0], outs[1]):
             assert torch.equal(x, y), K
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
-    monkeypatch.delenv("INVSIM_NV_ROLL")
 
 
 @pytest.mark.parametrize("graph,kw", [("default", dict(autoreset_mode="next_step")),
@@ -868,8 +859,9 @@ def test_net_demand_lookahead_mixed_calls(gpu, graph, kw, monkeypatch):
     from invsim.topology import custom_graph, default_graph
     mk_g = default_graph if graph == "default" else custom_graph
     n = 777
-    envs = [invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), num_periods=9, record_demand=True,
-                                       record_info=True, **kw) for _ in range(2)]
+    envs = knob_envs(monkeypatch, "INVSIM_NET_AHEAD", ("1", "0"),
+                     lambda: invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), num_periods=9,
+                                                        record_demand=True, record_info=True, **kw))
     A_dim = envs[0].action_dim
     g = torch.Generator(device=gpu).manual_seed(5)
     A = torch.rand((200, n, A_dim), device=gpu, generator=g) * 200 - 5
@@ -877,8 +869,7 @@ def test_net_demand_lookahead_mixed_calls(gpu, graph, kw, monkeypatch):
 
     def both(fn):
         outs = []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_NET_AHEAD", "1" if i == 0 else "0")
+        for env in envs:
             outs.append(fn(env))
         return outs
 
@@ -948,28 +939,20 @@ def test_invmgmt_three_role_rollout_equals_two_role(gpu, monkeypatch, cls, n, pe
     count: 32 768 envs, and 4 090 whose last group is partial; odd counts fall
     back to one group)."""
     import invsim
-    envs = []
-    for i in range(4):
-        env = getattr(invsim, cls)(n, device=gpu, record_demand=True, periods=periods)
+    mk = lambda: getattr(invsim, cls)(n, device=gpu, record_demand=True, periods=periods)  # noqa: E731
+    envs = [mk()]
+    for var, v in (("INVSIM_IM_ROLL3O_MAX_N", "0"), ("INVSIM_IM_ROLL", "0"), ("INVSIM_IM_ROLL3O_G2", "1")):
+        envs += knob_envs(monkeypatch, var, (v,), mk)
+    for env in envs:
         env.reset(seed=17)
-        envs.append(env)
     g = torch.Generator(device=gpu).manual_seed(3)
     for K in (75, 9, 2):
         a = torch.randint(-5, 260, (K, n, 3), device=gpu, dtype=torch.int64, generator=g)
         a[::3, ::89, 2] = (1 << 33) + 1         # wide requested orders, every third step
         outs, dems = [], []
-        for i, env in enumerate(envs):
-            if i == 1:
-                monkeypatch.setenv("INVSIM_IM_ROLL3O_MAX_N", "0")
-            if i == 2:
-                monkeypatch.setenv("INVSIM_IM_ROLL", "0")
-            if i == 3:
-                monkeypatch.setenv("INVSIM_IM_ROLL3O_G2", "1")
+        for env in envs:
             outs.append(env.rollout(a))
             dems.append(env._demand.clone())
-            monkeypatch.delenv("INVSIM_IM_ROLL3O_MAX_N", raising=False)
-            monkeypatch.delenv("INVSIM_IM_ROLL", raising=False)
-            monkeypatch.delenv("INVSIM_IM_ROLL3O_G2", raising=False)
         for j in (1, 2, 3):
             for x, y in zip(outs[0], outs[j]):
                 assert torch.equal(x, y), (K, j)
@@ -993,12 +976,12 @@ def test_net_three_role_rollout_equals_two_role(gpu, monkeypatch, graph, backlog
     import invsim
     from invsim.topology import custom_graph, default_graph
     mk_g = default_graph if graph == "default" else custom_graph
-    envs = []
-    for i in range(2):
-        env = invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), backlog=backlog, num_periods=periods,
-                                         autoreset_mode=mode, record_demand=True)
+    envs = knob_envs(monkeypatch, "INVSIM_NET_ROLL3", ("1", "0"),
+                     lambda: invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), backlog=backlog,
+                                                        num_periods=periods, autoreset_mode=mode,
+                                                        record_demand=True))
+    for env in envs:
         env.reset(seed=23)
-        envs.append(env)
     A = envs[0].action_dim
     g = torch.Generator(device=gpu).manual_seed(4)
     a = torch.rand((n, A), device=gpu, generator=g) * 250
@@ -1009,15 +992,13 @@ def test_net_three_role_rollout_equals_two_role(gpu, monkeypatch, graph, backlog
         a = torch.rand((K, n, A), device=gpu, generator=g) * 300 - 5
         a[:, ::53, 0] = 2.5                    # half-to-even ties
         outs, dems = [], []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_NET_ROLL3", "1" if i == 0 else "0")
+        for env in envs:
             outs.append(env.rollout(a))
             dems.append(env._demand.clone())
         for x, y in zip(outs[0], outs[1]):
             assert torch.equal(x, y), K
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
-    monkeypatch.delenv("INVSIM_NET_ROLL3")
 
 
 @pytest.mark.parametrize("family,cls_name,n", [
@@ -1137,24 +1118,22 @@ def test_newsvendor_rollout_sampler_mixes(gpu, monkeypatch, mu_max, step_limit):
     (up to 4 / 8 / 16 envs) and the one-lane fallback above 16."""
     import invsim
     n = 3000
-    envs = []
-    for i in range(2):
-        env = invsim.NewsvendorEnv(n, device=gpu, mu_max=mu_max, step_limit=step_limit, record_demand=True)
+    envs = knob_envs(monkeypatch, "INVSIM_NV_ROLL", ("1", "0"),
+                     lambda: invsim.NewsvendorEnv(n, device=gpu, mu_max=mu_max, step_limit=step_limit,
+                                                  record_demand=True))
+    for env in envs:
         env.reset(seed=77)
-        envs.append(env)
     g = torch.Generator(device=gpu).manual_seed(2)
     for K in (45, 8):
         a = torch.rand((K, n, 1), device=gpu, generator=g) * 300
         outs, dems = [], []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_NV_ROLL", "1" if i == 0 else "0")
+        for env in envs:
             outs.append(env.rollout(a))
             dems.append(env._demand.clone())
         for x, y in zip(outs[0], outs[1]):
             assert torch.equal(x, y), K
         assert torch.equal(dems[0], dems[1])
         assert torch.equal(envs[0].get_state(), envs[1].get_state()), K
-    monkeypatch.delenv("INVSIM_NV_ROLL")
 
 
 @pytest.mark.parametrize("graph,n", [("default", 1000), ("custom", 777), ("default", 32768)])
@@ -1166,8 +1145,9 @@ def test_net_two_wave_step_equals_one_wave(gpu, monkeypatch, graph, n):
     import invsim
     from invsim.topology import custom_graph, default_graph
     mk_g = default_graph if graph == "default" else custom_graph
-    envs = [invsim.NetInvMgmtBacklogEnv(n, device=gpu, graph=mk_g(), record_demand=True, record_info=True)
-            for _ in range(2)]
+    envs = knob_envs(monkeypatch, "INVSIM_NET_SPLIT", ("1", "0"),
+                     lambda: invsim.NetInvMgmtBacklogEnv(n, device=gpu, graph=mk_g(), record_demand=True,
+                                                         record_info=True))
     for env in envs:
         env.reset(seed=9)
     g = torch.Generator(device=gpu).manual_seed(4)
@@ -1175,15 +1155,13 @@ def test_net_two_wave_step_equals_one_wave(gpu, monkeypatch, graph, n):
     for k in range(65):
         a = torch.rand((n, A), device=gpu, generator=g) * 250 - 5
         outs = []
-        for i, env in enumerate(envs):
-            monkeypatch.setenv("INVSIM_NET_SPLIT", "1" if i == 0 else "0")
+        for env in envs:
             o, r, te, tr, info = env.step(a)
             outs.append([o.clone(), r.clone(), tr.clone(), env._demand.clone()]
                         + [v.clone() for v in info.values() if torch.is_tensor(v)])
         for x, y in zip(outs[0], outs[1]):
             assert torch.equal(x, y), k
     assert torch.equal(envs[0].get_state(), envs[1].get_state())
-    monkeypatch.delenv("INVSIM_NET_SPLIT")
 
 
 @pytest.mark.parametrize("dists", [("binomial", "binomial", "binomial"), ("integers", "integers", "integers"),
