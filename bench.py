@@ -335,9 +335,12 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     else:
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
+    # the closing barrier brackets the region on every rank; each rank's clock
+    # stops when its own work is done (not after the barrier's latency, which
+    # is tens of us over RCCL against a ~0.2 ms driver-style region), and the
+    # max over ranks below is the last rank's finish
     if dist.is_initialized():
         dist.barrier()
-        t1 = time.perf_counter()
     el = t1 - t0
     backend = dist.get_backend() if dist.is_initialized() else None
     cdev = dev if backend == "nccl" else torch.device("cpu")
@@ -377,6 +380,11 @@ def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
     N, O = env.num_envs, env.obs_dim
     C1 = env._horizon() + 1
     Q = max(1, min(4, 128 // C1, -(-steps // C1)))   # cycles per replay
+    # Newsvendor's demand lookahead flips its slot on step_limit - 1 launches of a
+    # cycle: with an odd count a replay of Q cycles would not start where it was
+    # recorded (invsim_capture_end refuses the capture), so Q is made even there
+    if env.family == invsim._capi.INVSIM_NEWSVENDOR and (C1 - 2) % 2 and Q % 2:
+        Q = Q + 1 if Q < 4 else Q - 1
     C = Q * C1
     pool = max(1, args.pool)
     acts = make_actions(env, pool, 0, gen)
@@ -415,9 +423,8 @@ def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
     e1.synchronize()
     t1 = time.perf_counter()
     torch.cuda.synchronize(dev)
-    if dist.is_initialized():
+    if dist.is_initialized():                 # bracket; each rank's clock stopped at its own end (above)
         dist.barrier()
-        t1 = time.perf_counter()
     el = t1 - t0
     if dist.is_initialized():
         cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
@@ -434,8 +441,8 @@ def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
             "episode_stats": dict(ep, source="the replays' own episode fold, one all-reduce after the region")}
 
 
-def _roofline(r, traffic, traffic_src):
-    return {"bound": "hbm", "achieved": r["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+def _roofline(r, traffic, traffic_src, rocprof=None, issue=None):
+    out = {"bound": "hbm", "achieved": r["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": r["achieved"] / HBM_PEAK_GBS,
             "frac_kernel": r["achieved"] / HBM_PEAK_GBS,
             "frac_wall": r["achieved_wall"] / HBM_PEAK_GBS,
@@ -446,7 +453,77 @@ def _roofline(r, traffic, traffic_src):
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": r["B"] * r["N"] * r["steps_per_call"],
             "bytes_per_env_step": r["B"], "kernel_ms_mean": r["kern_ms"],
-            "kernel_timing": "HIP events on the kernel stream around each block of launches / launches"}
+            "kernel_timing": "HIP events on the kernel stream around each block of launches / launches "
+                             "(every env-step launch: the dominant kernel and the NEXT_STEP reset launches)"}
+    if rocprof:
+        rocprof["event_over_all_launches"] = r["kern_ms"] * 1e6 / rocprof["all_step_launches_ns"]
+        out["rocprof"] = rocprof
+    if issue:
+        out["issue"] = issue
+    return out
+
+
+# invsim kernels that run env steps (a launch of invsim_step / _rollout /
+# _rollout_policy); the rest of a kernel-stats file is the episode fold, explicit
+# reset / seed kernels and torch's own kernels
+_STEP_KERNELS = ("_split_kernel", "_step1_kernel", "_step2_kernel", "_run_kernel", "_spec_kernel", "_roll",
+                 "_commit_kernel")
+
+
+def _newest(pattern):
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", pattern)))
+    return fs[-1] if fs else None
+
+
+def _rocprof(workload, mode, n_match, alg_bytes):
+    """The newest round's rocprofv3 kernel stats of this workload and mode
+    (profiles/rNN/<workload>_<mode>_kernel_stats.csv, the same bench command
+    under --kernel-trace --stats): the dominant kernel's mean duration and the
+    frac on it, and the mean over every env-step launch (the dominant kernel,
+    the NEXT_STEP reset launch, lookahead commits), which is what the HIP-event
+    figure averages."""
+    import csv
+    f = _newest(f"{workload}_{mode}_kernel_stats.csv")
+    if not f or not n_match:
+        return None
+    rows = [r for r in csv.DictReader(open(f))
+            if r["Name"].startswith(("void invsim::", "invsim::")) and any(k in r["Name"] for k in _STEP_KERNELS)]
+    if not rows:
+        return None
+    dom = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+    calls = sum(int(r["Calls"]) for r in rows)
+    mean_all = sum(float(r["TotalDurationNs"]) for r in rows) / calls
+    dom_ns = float(dom["AverageNs"])
+    return {"source": os.path.relpath(f, ROOT), "dominant_kernel": dom["Name"].split("(")[0].replace("void ", ""),
+            "dominant_ns": dom_ns, "dominant_share_of_launches": int(dom["Calls"]) / calls,
+            "frac_dominant": alg_bytes / dom_ns / HBM_PEAK_GBS,
+            "all_step_launches_ns": mean_all, "frac_all_launches": alg_bytes / mean_all / HBM_PEAK_GBS}
+
+
+def _issue(workload, mode, kern_ms):
+    """Issue-rate roofline of the Newsvendor kernels, whose bound is the
+    instruction stream, not HBM: VALU + SALU wave-instructions per
+    launch (SQ_INSTS_VALU + SQ_INSTS_SALU, newest profiles/rNN/sq_newsvendor.json)
+    over what 1 024 SIMDs issue in the launch's duration at the measured best
+    SIMD issue interval (v_add_u32 with four waves: 2.2 cycles,
+    profiles/r04/launch/valu_rates.txt) at 2.4 GHz."""
+    if workload != "newsvendor" or mode not in ("step", "rollout"):
+        return None
+    f = _newest("sq_newsvendor.json")
+    if not f:
+        return None
+    rec = json.load(open(f)).get(mode)
+    if not rec:
+        return None
+    c = rec["counters_mean_per_dispatch"]
+    insts = c["SQ_INSTS_VALU"] + c["SQ_INSTS_SALU"]
+    cap = 1024 * kern_ms * 1e-3 * 2.4e9 / 2.2
+    return {"bound": "issue", "instructions_per_launch": insts, "achieved": insts / (kern_ms * 1e-3),
+            "peak": 1024 * 2.4e9 / 2.2, "unit": "wave-instructions/s", "frac": insts / cap,
+            "source": os.path.relpath(f, ROOT),
+            "what": "VALU + SALU wave-instructions per launch (SQ) / (1024 SIMDs x launch cycles at 2.4 GHz / "
+                    "2.2 cycles per instruction)"}
 
 
 def _pmc(workload, mode, n_match):
@@ -529,7 +606,9 @@ def main():
                    "autoreset": "next_step",
                    "parallelism": f"dp{world} (env sharding, no data-path collective)",
                    "backend": (backend if dist.is_initialized() else None), "demand_stream": args.demand_stream},
-        "roofline": _roofline(r, traffic, traffic_src),
+        "roofline": _roofline(r, traffic, traffic_src,
+                              _rocprof(args.workload, args.mode, full, r["B"] * N * r["steps_per_call"]),
+                              _issue(args.workload, args.mode, r["kern_ms"])),
         "episode_stats": dict(r["ep"], source="timed batch: HIP episode fold of the timed steps' rewards and "
                                               "done flags, one all-reduce after the region"),
     }
@@ -551,7 +630,9 @@ def main():
         out["rollout"] = {"value": rr["total_steps"] * N * world / rr["el"], "unit": "env-steps/s",
                           "steps": rr["total_steps"], "launches": rr["calls"], "K": rr["K"],
                           "ms_per_launch": rr["el"] * 1e3 / rr["calls"],
-                          "roofline": _roofline(rr, t2, s2),
+                          "roofline": _roofline(rr, t2, s2,
+                                                _rocprof(args.workload, "rollout", full, rr["B"] * N * rr["K"]),
+                                                _issue(args.workload, "rollout", rr["kern_ms"])),
                           "episode_stats": dict(rr["ep"], cycles=rr["total_steps"] // C,
                                                 source="timed rollout batch: HIP episode fold between "
                                                        "launch blocks, one all-reduce after the region")}

@@ -26,13 +26,17 @@ struct Pcg {
     uint64_t inc_hi, inc_lo;  // 128-bit increment (odd)
 
     __device__ __forceinline__ uint64_t next64() {
-        // state = state * MULT + inc  (mod 2^128)
-        uint64_t nlo = lo * PCG_MULT_LO;
-        uint64_t nhi = __umul64hi(lo, PCG_MULT_LO) + lo * PCG_MULT_HI + hi * PCG_MULT_LO;
-        uint64_t slo = nlo + inc_lo;
-        nhi += inc_hi + (slo < nlo ? 1ULL : 0ULL);
-        hi = nhi;
-        lo = slo;
+        // state = state * MULT + inc  (mod 2^128).  As one 128-bit multiply-add
+        // the compiler emits six v_mad_u64_u32 + four v_mul_lo_u32 and an
+        // add-with-carry chain for the increment: ~25 instructions against ~29
+        // for the 64-bit-halves form (__umul64hi).  A lone stream wave issues one
+        // instruction per ~9 cycles whatever its dependencies, so
+        // the instruction count is the step's cost.
+        typedef unsigned __int128 u128;
+        u128 st = ((u128)hi << 64) | lo;
+        st = st * (((u128)PCG_MULT_HI << 64) | PCG_MULT_LO) + (((u128)inc_hi << 64) | inc_lo);
+        hi = (uint64_t)(st >> 64);
+        lo = (uint64_t)st;
         uint64_t x = hi ^ lo;
         unsigned rot = (unsigned)(hi >> 58);
         return (x >> rot) | (x << ((64u - rot) & 63u));
@@ -296,43 +300,71 @@ __device__ __forceinline__ bool ptrs_log_accept(const PtrsConst &c, double V, do
 // One numpy PTRS candidate (the loop body of random_poisson_ptrs) from its two
 // uniforms, with the same decision as the branchy form above, laid out for a
 // lone wave: its three chains -- k (the f64 division and floor), the f32 log
-// test's inputs (us, V only) and the RHS table read (k only) -- are computed
-// for every lane without branches between them, so they interleave instead of
-// running one after the other; only a near-tie of the f32 test, x/us overflow
-// or k outside the table take the exact branch.  The f32 x = a/us^2 + b uses
-// v_rcp_f32 (1 ulp): relative error <= 10 * 2^-24, i.e. <= 2^-20 in log2,
-// within the input allowance of ptrs_log_accept's bound.
-// tab(k, ok): -lam + k log lam - loggam(k + 1) from an LDS table (ok = false:
-// k outside it, value unused); rhs(k): the same, exactly, on device.
+// test (us, V only) and the RHS table read (k only) -- are computed for every
+// lane without branches between them, so they interleave instead of running
+// one after the other; only a near-tie of the f32 test, x/us overflow or k
+// outside the table take the exact branch.
+//
+// The fast test runs in f32 end to end (round 5: 9 f32 instructions where the
+// f64 combination took ~17; a stream wave's cost is its instruction count).
+// With l2v = log2f(fl(V)), l2x = log2f(x32), x32 = a * rcp(us^2) + b in f32,
+// and every f32 rounding counted (d = l2v - l2x, L = fma(d, ln2, log_invalpha),
+// the f32 ln2, log_invalpha and r, diff = r - L):
+//   |diff - (r - lhs)| <= ln2 (|l2v| + |l2x|) (2^-22 + 4 * 2^-24)   [log2f 4 ulp + roundings]
+//                       + ln2 * 2^-19                                 [V, x input roundings]
+//                       + 3 * 2^-24 |log_invalpha| + 2 * 2^-24 |r| + 2^-24 |diff|
+// which  e = (|l2v| + |l2x|) 2^-20 + |r| 2^-22 + (2^-18 + 2^-22 |log_invalpha|)
+// bounds with a factor >= 2 to spare (that slack also covers e's own f32
+// roundings): diff > e decides accept, diff < -e reject, as numpy's f64 test.
+// tab(kd, ok): -lam + kd log lam - loggam(kd + 1) from an LDS table for the
+// candidate's floor value kd (ok = false: kd outside it, value unused);
+// rhs(k): the same, exactly, on device.
+// ptrs_decide_d hands back the candidate as its floor value kd, a double
+// (numpy's k is (int64)kd, and kd is integral, so nothing is lost): a caller
+// that keeps the draw as a double skips the int64 conversion per candidate.
 template <class Tab, class Rhs>
-__device__ __forceinline__ bool ptrs_decide(const PtrsConst &c, double U, double V, Tab tab, Rhs rhs, int64_t &k) {
-    constexpr double LN2 = 0.69314718055994530942;
+__device__ __forceinline__ bool ptrs_decide_d(const PtrsConst &c, double U, double V, Tab tab, Rhs rhs, double &kd) {
     const double us = 0.5 - fabs(U);
-    k = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+    kd = floor((c.a2 / us + c.b) * U + c.lam + 0.43);
     const float us32 = (float)us;
     const float x32 = (float)c.a * __builtin_amdgcn_rcpf(us32 * us32) + (float)c.b;
     const float l2v = __builtin_amdgcn_logf((float)V);
     const float l2x = __builtin_amdgcn_logf(x32);
     bool ok;
-    const double r = tab(k, ok);
-    const bool qacc = (us >= 0.07) && (V <= c.vr);
-    const bool qrej = (k < 0) || ((us < 0.013) && (V > us));
-    const double lhs = ((double)l2v * LN2 + c.log_invalpha) - (double)l2x * LN2;
-    const double err = (fabs((double)l2v) + fabs((double)l2x)) * (LN2 * 0x1p-22) + LN2 * 0x1p-19 +
-                       (fabs(lhs) + fabs(r)) * 0x1p-40;
-    const bool fin = ok && (x32 < 1e30f);
-    const bool facc = fin && (lhs + err < r), frej = fin && (lhs - err > r);
+    const double r = tab(kd, ok);      // kd == (double)k wherever the table is read (0 <= k < 2^53)
+    // bitwise, not short-circuit, here and below: no branch per condition
+    const bool qacc = (us >= 0.07) & (V <= c.vr);
+    const bool qrej = (kd < 0.0) | ((us < 0.013) & (V > us));     // k < 0 (kd is never NaN; -inf: k < 0 too)
+    const float lia = (float)c.log_invalpha;
+    const float r32 = (float)r;
+    const float L = __builtin_fmaf(l2v - l2x, 0.693147180559945309f, lia);
+    const float diff = r32 - L;
+    const float e = __builtin_fmaf(fabsf(l2v) + fabsf(l2x), 0x1p-20f,
+                                   __builtin_fmaf(fabsf(r32), 0x1p-22f, __builtin_fmaf(fabsf(lia), 0x1p-22f, 0x1p-18f)));
+    const bool fin = ok & (x32 < 1e30f);
+    const bool facc = fin & (diff > e), frej = fin & (diff < -e);
 #ifdef INVSIM_PTRS_STATS
     if (!qacc && !qrej && (facc || frej)) {   // f32-decided: count and check against the f64 test
-        const bool exact = (log(V) + c.log_invalpha - log(c.a / (us * us) + c.b)) <= r;
+        const double lhs64 = log(V) + c.log_invalpha - log(c.a / (us * us) + c.b);
+        const bool exact = lhs64 <= r;
+        const double margin = fabs(lhs64 - r) / (fabs(log(V)) + fabs(c.log_invalpha) +
+                                                 fabs(log(c.a / (us * us) + c.b)) + fabs(r));
         atomicAdd(&g_ptrs_stats[0], 1ull);
         if (facc != exact) atomicAdd(&g_ptrs_stats[3], 1ull);
+        atomicMin(&g_ptrs_stats[2], (unsigned long long)__double_as_longlong(margin));
     }
 #endif
-    // bitwise, not short-circuit: every lane computes every chain (no branch to sink them under)
     const bool dec = qacc | qrej | facc | frej;
     bool acc = qacc | (!qrej & facc);
-    if (!dec) acc = ptrs_log_accept(c, V, us, ok ? r : rhs(k));   // rare: the exact path
+    if (!dec) acc = ptrs_log_accept(c, V, us, ok ? r : rhs((int64_t)kd));   // rare: the exact path
+    return acc;
+}
+
+template <class Tab, class Rhs>
+__device__ __forceinline__ bool ptrs_decide(const PtrsConst &c, double U, double V, Tab tab, Rhs rhs, int64_t &k) {
+    double kd;
+    const bool acc = ptrs_decide_d(c, U, V, tab, rhs, kd);
+    k = (int64_t)kd;
     return acc;
 }
 

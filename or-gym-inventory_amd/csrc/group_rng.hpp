@@ -172,6 +172,11 @@ struct RhsTab {   // host table of the whole right-hand side for k in [c.k0, c.k
         ok = k >= c.k0 && k < (int64_t)c.k0 + c.nk;
         return t[ok ? (int)(k - c.k0) : 0];
     }
+    // the same for a candidate's floor value kd (ptrs_decide)
+    __device__ __forceinline__ double fastd(double kd, const PtrsConst &c, bool &ok) const {
+        ok = (kd >= (double)c.k0) & (kd < (double)(c.k0 + c.nk));
+        return t[ok ? (int)kd - c.k0 : 0];
+    }
     __device__ __forceinline__ double exact(int64_t k, const PtrsConst &c) const { return ptrs_rhs(c, nullptr, k); }
 };
 // (LgTab, the Newsvendor table source, is in kernels.hpp beside RHS_LDS_MAX)
@@ -187,7 +192,7 @@ __device__ __forceinline__ bool ptrs_candidate(G &g, const PtrsConst &c, const S
     const double V = g.next_double();
 #if INVSIM_PTRS_DECIDE
     return ptrs_decide(
-        c, U, V, [&](int64_t kk, bool &ok) { return src.fast(kk, c, ok); },
+        c, U, V, [&](double kd, bool &ok) { return src.fastd(kd, c, ok); },
         [&](int64_t kk) { return src.exact(kk, c); }, k);
 #else
     const double us = 0.5 - fabs(U);

@@ -261,6 +261,11 @@ struct LgTab {    // loggam(k + 1) for k < RHS_LDS_MAX (Newsvendor's per-episode
         ok = k >= 0 && k < RHS_LDS_MAX;
         return (-c.lam + (double)k * c.loglam) - lg[ok ? (int)k : 0];
     }
+    // the same for a candidate's floor value kd (ptrs_decide): no int64 -> f64 conversion
+    __device__ __forceinline__ double fastd(double kd, const PtrsConst &c, bool &ok) const {
+        ok = (kd >= 0.0) & (kd < (double)RHS_LDS_MAX);
+        return (-c.lam + kd * c.loglam) - lg[ok ? (int)kd : 0];
+    }
     __device__ __forceinline__ double exact(int64_t k, const PtrsConst &c) const {
         return -c.lam + (double)k * c.loglam - np_loggam((double)(k + 1));
     }

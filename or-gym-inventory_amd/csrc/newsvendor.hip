@@ -817,10 +817,11 @@ __device__ __forceinline__ void nv_chunk(int t, int rem, int step_limit, bool nx
 // finish one draw and start the next) -- and the group's base state advances
 // by the uniforms actually consumed.  Owners (lanes with `own`) hand their
 // generator to the group and get it back advanced; the group's first lane
-// writes the draws into the owner's column of `dcol` ([CH][WAVE]).
+// writes the draws into the owner's column of `dcol` ([CH][WAVE], as doubles:
+// the rollout's demand handoff rows hold every draw as a double, see nv_roll_kernel).
 // G = 16, 8 or 4 for up to 4, 8 or 16 envs; more than 16 envs (small mu_max)
 // keep the one-lane sequential sampler (the caller's fallback): returns false.
-__device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own, int nd, int64_t *dcol,
+__device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own, int nd, double *dcol,
                                                   double *ubuf, const uint64_t *jt, int lane) {
     const uint64_t mm = (uint64_t)__ballot(own && nd > 0);
     const int nm = __popcll(mm);
@@ -884,7 +885,7 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
         while (__ballot(stops != 0 && need > 0)) {
             if (stops != 0 && need > 0) {
                 const int pos = __builtin_ctz(stops);
-                if (jl == 0) dcol[j * WAVE + src] = (int64_t)(last < 0 ? X + pos : pos - last - 1);
+                if (jl == 0) dcol[j * WAVE + src] = (double)(last < 0 ? X + pos : pos - last - 1);
                 j++;
                 need--;
                 last = pos;
@@ -972,7 +973,7 @@ struct NvRoll {
 // nv_run_kernel<..., PhiloxGen> (test_fast_stream_newsvendor_fused_kernels_...).
 template <int LT>
 __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int lane, int64_t e, int64_t el, bool valid,
-                                             int t_start, int K, bool nxt, double *lg_l, int64_t *dbuf,
+                                             int t_start, int K, bool nxt, double *lg_l, double *dbuf,
                                              double *pbuf, uint64_t *kb) {
     constexpr int CH = NvRoll<LT>::CH, NP = NvRoll<LT>::NP;
     const int64_t S = P.cm.Npad;
@@ -994,7 +995,7 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
         bool rs;
         nv_chunk(t, K - k0, P.step_limit, nxt, NvRoll<LT>::CH, len, rs);
         const int nd = len - (rs ? 1 : 0);                   // the reset step draws none
-        int64_t *dcol = dbuf + cb * CH * WAVE;
+        double *dcol = dbuf + cb * CH * WAVE;
         const uint64_t ph0 = P.cm.ph_step + (uint64_t)k0;    // launch step of the chunk's first step
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
         for (int j = role; j < nd; j += 2) dcol[j * WAVE + lane] = 20;
@@ -1017,7 +1018,7 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
                     acc = ptrs_log_accept(c, V, us, r);
                 }
                 if (acc) {
-                    dcol[j * WAVE + lane] = kd;
+                    dcol[j * WAVE + lane] = (double)kd;   // exact: kd is the floor of a double
                     j += 2;
                     cj = 0;
                 } else {
@@ -1045,7 +1046,7 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
                     g.key = make_uint2((uint32_t)kk, (uint32_t)(kk >> 32));
                     g.set_step(ph0 + (uint64_t)j);
                     g.sub(0);
-                    dcol[j * WAVE + src] = np_poisson_mult(g, __longlong_as_double((long long)kw[WAVE + src]));
+                    dcol[j * WAVE + src] = (double)np_poisson_mult(g, __longlong_as_double((long long)kw[WAVE + src]));
                 }
                 wave_lds_sync();
             }
@@ -1126,7 +1127,10 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     extern __shared__ __attribute__((aligned(16))) float nr_lds[];
     float *tile = nr_lds;
     double *lg_l = reinterpret_cast<double *>(nr_lds + R::tile_bytes() / sizeof(float));
-    int64_t *dbuf = reinterpret_cast<int64_t *>(lg_l + RHS_LDS_MAX);     // [2][CH][WAVE]
+    // [2][CH][WAVE] demands as doubles: a PTRS draw is the floor value of a
+    // double (numpy's k = (int64)kd), so the stream wave stores kd as it is and
+    // the dynamics wave converts, off the PTRS wave's per-candidate path
+    double *dbuf = lg_l + RHS_LDS_MAX;
     double *pbuf = reinterpret_cast<double *>(dbuf + 2 * CH * WAVE);      // [2][NP][WAVE]
     double *ubuf = pbuf + 2 * NP * WAVE;                                   // [WAVE] mult wave's uniforms
     uint64_t *jt = reinterpret_cast<uint64_t *>(ubuf + WAVE);              // [4][JUMP_MAX + 1] jump table
@@ -1178,7 +1182,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             bool rs;
             nv_chunk(t, K - k0, P.step_limit, nxt, CH, len, rs);
             const int nd = mine ? len - (rs ? 1 : 0) : 0;    // draws of this env (the reset step draws none)
-            int64_t *db = dbuf + cb * CH * WAVE + lane;
+            double *db = dbuf + cb * CH * WAVE + lane;
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
             for (int j = 0; j < nd; j++) db[j * WAVE] = 20;
 #else
@@ -1205,20 +1209,21 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
 #endif
                         const double U = st.g.next_double() - 0.5;
                         const double V = st.g.next_double();
-                        int64_t kd;
+                        double kd;
 #if INVSIM_PTRS_DECIDE
                         const LgTab src{lg_l};
-                        const bool acc = ptrs_decide(
-                            c, U, V, [&](int64_t kk, bool &ok) { return src.fast(kk, c, ok); },
+                        const bool acc = ptrs_decide_d(
+                            c, U, V, [&](double kd, bool &ok) { return src.fastd(kd, c, ok); },
                             [&](int64_t kk) { return src.exact(kk, c); }, kd);
 #else
                         const double us = 0.5 - fabs(U);
-                        kd = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+                        const int64_t ki = (int64_t)floor((c.a2 / us + c.b) * U + c.lam + 0.43);
+                        kd = (double)ki;
                         bool acc = (us >= 0.07) && (V <= c.vr);
-                        if (!acc && !((kd < 0) || ((us < 0.013) && (V > us)))) {
-                            const double r = (kd < RHS_LDS_MAX)
-                                                 ? (-c.lam + (double)kd * c.loglam) - lg_l[kd < RHS_LDS_MAX ? kd : 0]
-                                                 : -c.lam + (double)kd * c.loglam - np_loggam((double)(kd + 1));
+                        if (!acc && !((ki < 0) || ((us < 0.013) && (V > us)))) {
+                            const double r = (ki < RHS_LDS_MAX)
+                                                 ? (-c.lam + (double)ki * c.loglam) - lg_l[ki < RHS_LDS_MAX ? ki : 0]
+                                                 : -c.lam + (double)ki * c.loglam - np_loggam((double)(ki + 1));
                             acc = ptrs_log_accept(c, V, us, r);
                         }
 #endif
@@ -1241,7 +1246,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                     if (prod > c.enlam) {
                         X += 1;
                     } else {
-                        db[j * WAVE] = X;
+                        db[j * WAVE] = (double)X;
                         j++;
                         X = 0;
                         prod = 1.0;
@@ -1429,7 +1434,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 else act = pol.cf[0];
                 if (valid && pol.act_out) out_store((float *)pol.act_out + oi, act);
             }
-            const int64_t d = dbuf[(cb * CH + kk) * WAVE + lane];
+            const int64_t d = (int64_t)dbuf[(cb * CH + kk) * WAVE + lane];
             double r;
             nv_step_regs<LT>(P, e, valid, sc, st, act, nullptr, lg_l, nullptr, r, nullptr, d,
                              (valid && k == K - 1) ? (double *)P.cm.info_rec : nullptr, false);

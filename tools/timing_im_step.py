@@ -2,7 +2,7 @@
 demand lookahead): lookahead workgroups vs the step's window and dynamics
 waves (profiling only; needs the TIMING build, csrc `make timing`).
 
-  INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so python tools/timing_im_step.py
+  INVSIM_LIB=or-gym-inventory_amd/invsim/_lib/ablate/libinvsim_TIMING.so python tools/timing_im_step.py [N] [lostsales]
 
 Probes (s_memrealtime, 100 MHz): 0 workgroup entry (thread 0); lookahead
 1 loads + RHS table in LDS, 2 demand drawn, 5 exit; step 3 / 4 dynamics wave
@@ -24,7 +24,8 @@ def main():
     import invsim
     from invsim import _capi
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-    env = invsim.InvManagementBacklogEnv(num_envs=n)
+    cls = invsim.InvManagementLostSalesEnv if "lostsales" in sys.argv[2:] else invsim.InvManagementBacklogEnv
+    env = cls(num_envs=n)
     env.reset(seed=0)
     g = torch.Generator(device="cuda").manual_seed(1)
     hi = torch.as_tensor(env.single_action_space.high, device=env.device)
