@@ -495,7 +495,9 @@ def _rocprof(workload, mode, n_match, alg_bytes):
     calls = sum(int(r["Calls"]) for r in rows)
     mean_all = sum(float(r["TotalDurationNs"]) for r in rows) / calls
     dom_ns = float(dom["AverageNs"])
-    return {"source": os.path.relpath(f, ROOT), "dominant_kernel": dom["Name"].split("(")[0].replace("void ", ""),
+    import re
+    m = re.search(r"(\w+_kernel)", dom["Name"])
+    return {"source": os.path.relpath(f, ROOT), "dominant_kernel": m.group(1) if m else dom["Name"][:80],
             "dominant_ns": dom_ns, "dominant_share_of_launches": int(dom["Calls"]) / calls,
             "frac_dominant": alg_bytes / dom_ns / HBM_PEAK_GBS,
             "all_step_launches_ns": mean_all, "frac_all_launches": alg_bytes / mean_all / HBM_PEAK_GBS}

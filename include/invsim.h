@@ -255,9 +255,11 @@ int invsim_episode_fold(const double *reward, const uint8_t *terminated, const u
 
 /* Debug builds only (make -C csrc ptrs_stats -> invsim/_lib/debug/): PTRS
  * log-acceptance statistics since the last clear, summed over kernels:
- * out[0] log tests, out[1] tests the f64 fallback decided, out[2] bit pattern
- * of the smallest relative margin |lhs - rhs| / (sum of |terms|) (f64),
- * out[3] f32-decided tests that disagree with the f64 test.  Synchronises the
+ * out[0] log tests, out[1] tests ptrs_log_accept's f32 pre-test left to f64,
+ * out[2] bit pattern of the smallest relative margin |lhs - rhs| / (sum of
+ * |terms|) (f64), out[3] f32-decided tests that disagree with the f64 test,
+ * out[4] log tests the decide path's own f32 test (ptrs_decide_d) left to
+ * the exact branch (0 in a branchy build).  out has 5 words.  Synchronises the
  * device.  The product build returns INVSIM_EINVAL.  (No reference
  * equivalent: evidence for the numpy random_poisson_ptrs restatement,
  * distributions.c, SURVEY App. B.) */

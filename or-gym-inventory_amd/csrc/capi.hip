@@ -1083,16 +1083,17 @@ int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear) {
 #ifdef INVSIM_PTRS_STATS
     hipError_t (*tus[6])(unsigned long long *, bool) = {ptrs_stats_nv, ptrs_stats_nv_ph, ptrs_stats_im,
                                                         ptrs_stats_im_ph, ptrs_stats_netspec, ptrs_stats_net};
-    out[0] = out[1] = out[3] = 0;
+    out[0] = out[1] = out[3] = out[4] = 0;
     out[2] = 0x7ff0000000000000ull;
     for (auto f : tus) {
-        unsigned long long v[4];
+        unsigned long long v[5];
         hipError_t e = hipDeviceSynchronize();
         if (e == hipSuccess) e = f(v, clear != 0);
         if (e != hipSuccess) return hip_fail(nullptr, e, "ptrs stats");
         out[0] += v[0];
         out[1] += v[1];
         out[3] += v[3];
+        out[4] += v[4];
         out[2] = std::min<uint64_t>(out[2], v[2]);
     }
     return INVSIM_OK;

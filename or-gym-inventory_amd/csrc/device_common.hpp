@@ -242,16 +242,18 @@ __device__ __forceinline__ double ptrs_rhs(const PtrsConst &c, const double *rhs
 // overflow) evaluate the f64 logs.  Same decision as the f64 test.
 #ifdef INVSIM_PTRS_STATS
 // Debug build only (make ptrs_stats): per translation unit, [0] log tests,
-// [1] tests decided by the f64 fallback, [2] bits of the smallest relative
-// margin |lhs - r| / (|log V| + |log(1/alpha)| + |log x| + |r|) over all tests
-// (non-negative doubles order like their bit patterns), [3] f32 decisions that
-// disagree with the f64 test (must stay 0).  Read by invsim_debug_ptrs_stats.
-static __device__ unsigned long long g_ptrs_stats[4] = {0ull, 0ull, 0x7ff0000000000000ull, 0ull};
+// [1] tests ptrs_log_accept's f32 pre-test left to f64, [2] bits of the
+// smallest relative margin |lhs - r| / (|log V| + |log(1/alpha)| + |log x| + |r|)
+// over all tests (non-negative doubles order like their bit patterns), [3] f32
+// decisions that disagree with the f64 test (must stay 0), [4] log tests the
+// decide path's f32 test (ptrs_decide_d) left to the exact branch.  Read by
+// invsim_debug_ptrs_stats.
+static __device__ unsigned long long g_ptrs_stats[5] = {0ull, 0ull, 0x7ff0000000000000ull, 0ull, 0ull};
 #define INVSIM_PTRS_STATS_TU(tu)                                                                   \
     hipError_t ptrs_stats_##tu(unsigned long long *out, bool clear) {                              \
         hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptrs_stats), sizeof(g_ptrs_stats));   \
         if (e != hipSuccess || !clear) return e;                                                   \
-        const unsigned long long init[4] = {0ull, 0ull, 0x7ff0000000000000ull, 0ull};              \
+        const unsigned long long init[5] = {0ull, 0ull, 0x7ff0000000000000ull, 0ull, 0ull};        \
         return hipMemcpyToSymbol(HIP_SYMBOL(g_ptrs_stats), init, sizeof(init));                    \
     }
 
@@ -355,6 +357,9 @@ __device__ __forceinline__ bool ptrs_decide_d(const PtrsConst &c, double U, doub
     }
 #endif
     const bool dec = qacc | qrej | facc | frej;
+#ifdef INVSIM_PTRS_STATS
+    if (!dec) atomicAdd(&g_ptrs_stats[4], 1ull);
+#endif
     bool acc = qacc | (!qrej & facc);
     if (!dec) acc = ptrs_log_accept(c, V, us, ok ? r : rhs((int64_t)kd));   // rare: the exact path
     return acc;

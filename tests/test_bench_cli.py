@@ -52,3 +52,22 @@ def test_episode_stats_block_fold_host():
     assert np.allclose(st.acc.numpy(), acc, rtol=1e-12)
     res = st.allreduce()
     assert res["episodes"] == acc[2] and res["reward_sum"] == pytest.approx(acc[3])
+
+
+def test_roofline_rocprof_reconciliation_fields():
+    """the line's frac is reproduced from the committed
+    rocprof kernel stats: the dominant kernel's mean and the mean over every
+    env-step launch (what the HIP-event figure averages), read from the newest
+    profiles/rNN/<workload>_<mode>_kernel_stats.csv."""
+    import bench
+    alg = 746 * 65536
+    r = bench._rocprof("invmgmt_backlog", "step", True, alg)
+    assert r is not None and r["source"].startswith("profiles/r")
+    assert r["dominant_kernel"] == "im_split_kernel"
+    assert 0.9 < r["dominant_share_of_launches"] < 1.0          # the reset launch every 31 steps
+    assert r["all_step_launches_ns"] < r["dominant_ns"]            # the reset launch is cheaper
+    assert abs(r["frac_dominant"] - alg / r["dominant_ns"] / 8000.0) < 1e-12
+    assert bench._rocprof("invmgmt_backlog", "step", False, alg) is None   # another batch size: no file applies
+    i = bench._issue("newsvendor", "rollout", 0.06)
+    assert i["bound"] == "issue" and 0 < i["frac"] < 1 and i["instructions_per_launch"] > 1e6
+    assert bench._issue("invmgmt_backlog", "step", 0.009) is None

@@ -96,11 +96,11 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert d["ranks"] == 2
 
 
-def _bench_spawned(extra):
+def _bench_spawned(extra, rollout=False):
     """plain `bench.py --gpus 2` (no torchrun around it): bench.py starts the ranks"""
     env = dict(os.environ, INVSIM_BENCH_BACKEND="gloo")
     env.pop("WORLD_SIZE", None)
-    cmd = [sys.executable, "bench.py", "--gpus", "2", "--warmup", "5", "--no-rollout-line"] + extra
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--warmup", "5"] + ([] if rollout else ["--no-rollout-line"]) + extra
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     return _last_json(p.stdout)
@@ -116,10 +116,19 @@ def test_bench_gpus_flag_starts_ranks_weak():
 
 
 def test_bench_gpus_flag_strong_net():
-    d = _bench_spawned(["--steps", "20", "--workload", "net_backlog", "--strong"])
+    """--strong (config 5: 32 768 Net envs split over the ranks).  The per-rank
+    step is latency-bound at these sizes, so the line carries the
+    modes that hold up beside the eager one: the fused K=30 rollout (the
+    highest absolute rate) and the StepGraph replay, both over the same
+    per-rank shard and timed the same way."""
+    d = _bench_spawned(["--steps", "20", "--workload", "net_backlog", "--strong"], rollout=True)
     _check_line(d, 2, 20, 5)
     assert d["scaling"] == "strong" and d["ranks"] == 2
     assert d["config"]["envs_per_gpu"] == 16384 and d["config"]["global_envs"] == 32768
+    ro, gr = d["rollout"], d["graph"]
+    assert ro["K"] == 30 and ro["value"] > d["value"] and 0 < ro["roofline"]["frac"] < 1.5
+    assert ro["episode_stats"]["episodes"] == ro["episode_stats"]["cycles"] * 32768
+    assert gr["value"] > 0 and gr["steps"] % 31 == 0
 
 
 @pytest.mark.parametrize("wl", ["invmgmt_backlog", "newsvendor", "net_backlog"])

@@ -28,13 +28,13 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def stats(lib, clear):
-    out = (np.zeros(4, np.uint64))
+    out = (np.zeros(5, np.uint64))
     rc = lib.invsim_debug_ptrs_stats(out.ctypes.data, 1 if clear else 0)
     if rc:
         raise RuntimeError("invsim_debug_ptrs_stats failed: not the PTRS-statistics build?")
     margin = struct.unpack("<d", struct.pack("<Q", int(out[2])))[0]
     return dict(log_tests=int(out[0]), f64_fallbacks=int(out[1]), min_rel_margin=margin,
-                f32_disagreements=int(out[3]))
+                f32_disagreements=int(out[3]), decide_f32_undecided=int(out[4]))
 
 
 def main():
@@ -65,7 +65,8 @@ def main():
                       lambda env, cyc=cyc, n=n: _pool_f32(np.random.default_rng(cyc), 31, n, env.action_dim, 150.0),
                       31 * cyc, mode, 3000 + cyc, n * 30 * cyc * (1 if graph == "default" else 3)))
     res = []
-    tot = dict(log_tests=0, f64_fallbacks=0, f32_disagreements=0, min_rel_margin=float("inf"), draws=0)
+    tot = dict(log_tests=0, f64_fallbacks=0, f32_disagreements=0, decide_f32_undecided=0,
+               min_rel_margin=float("inf"), draws=0)
     for name, mk, pool_np, T, mode, seed, draws in cases:
         env = mk()
         if callable(pool_np):
@@ -80,7 +81,7 @@ def main():
         s.update(path=name, draws=draws, seconds=round(time.time() - t0, 2))
         res.append(s)
         print(json.dumps(s), file=sys.stderr, flush=True)
-        for k in ("log_tests", "f64_fallbacks", "f32_disagreements", "draws"):
+        for k in ("log_tests", "f64_fallbacks", "f32_disagreements", "decide_f32_undecided", "draws"):
             tot[k] += s[k]
         tot["min_rel_margin"] = min(tot["min_rel_margin"], s["min_rel_margin"])
         env.close()
