@@ -999,13 +999,19 @@ constexpr int IM_AP_LDS = 256;   // alpha**t LDS table of the 3-role rollout (pe
 #define IM_ROLL3O_STAGE 0
 #endif
 
+#ifndef IM_ROLL3_CH
+#define IM_ROLL3_CH 8
+#endif
+#ifndef IM_ROLL3_RD
+#define IM_ROLL3_RD 4
+#endif
 template <int L0, int L1, int L2>
 struct ImLt3 {
     static constexpr int M1 = 3;
     static constexpr int D = (L0 > L1 ? (L0 > L2 ? L0 : L2) : (L1 > L2 ? L1 : L2));
     static constexpr int O = M1 * (D + 1);
-    static constexpr int CH = 8;                                         // demand chunk (launch steps)
-    static constexpr int RD = 4;                                         // demand ring depth (chunks)
+    static constexpr int CH = IM_ROLL3_CH;                               // demand chunk (launch steps)
+    static constexpr int RD = IM_ROLL3_RD;                               // demand ring depth (chunks)
     static constexpr int lt(int i) { return i == 0 ? L0 : i == 1 ? L1 : L2; }
     static constexpr int W(int i) { return lt(i) > 0 ? lt(i) : 1; }      // register window length
     static constexpr size_t lds() {

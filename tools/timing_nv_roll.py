@@ -108,6 +108,22 @@ def main():
             print(f"  {name:12s} trips {fmt(tr / 10.0)}")
             print(f"  {'':12s} ns/trip {fmt(work[ok] / tr[ok])}")
     print(f"kernel span {(b[:, 6].max() - t0) * 10.0:.0f} ns")
+    if layout == "L0":
+        # the tail: the workgroups that end last, which role ends them, and how
+        # many multiplication-branch envs (mu < 10) they hold after the launch
+        ends = b[:, 6].reshape(-1, R)
+        wg_end = ends.max(axis=1) - t0
+        mu = env.params()[:, 4].cpu().numpy()[: (n // 64) * 64].reshape(-1, 64)
+        nm = (mu < 10).sum(axis=1)
+        order = np.argsort(wg_end)
+        for label, sel in (("slowest 2 %", order[-len(order) // 50:]), ("median 50 %", order[len(order) // 4: 3 * len(order) // 4])):
+            last = np.bincount(ends[sel].argmax(axis=1), minlength=R)
+            print(f"  {label} of workgroups: end {np.percentile(wg_end[sel], 50) * 10.0:.0f} ns (p50); "
+                  f"last role " + ", ".join(f"{name} {last[r]}" for r, name in roles) +
+                  f"; mult envs p50 {np.percentile(nm[sel], 50):.0f} max {nm[sel].max()}")
+            if len(trip) and trip.any():
+                print(f"  {'':12s} PTRS trips p50 {np.percentile(trip[0::R][sel], 50):.1f}, "
+                      f"mult rounds p50 {np.percentile(trip[1::R][sel], 50):.1f}")
 
 
 if __name__ == "__main__":
