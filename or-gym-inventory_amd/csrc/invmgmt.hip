@@ -999,8 +999,12 @@ constexpr int IM_AP_LDS = 256;   // alpha**t LDS table of the 3-role rollout (pe
 #define IM_ROLL3O_STAGE 0
 #endif
 
+// demand chunk of im_roll3_kernel: 4 launch steps (round 5; 65 536 envs, K = 30:
+// 108.0-109.0 us against 112.1-113.0 with 8, equal at 262 144 envs,
+// profiles/r05/roll3_ring/ab.txt; a smaller first chunk starts the dynamics
+// wave sooner)
 #ifndef IM_ROLL3_CH
-#define IM_ROLL3_CH 8
+#define IM_ROLL3_CH 4
 #endif
 #ifndef IM_ROLL3_RD
 #define IM_ROLL3_RD 4

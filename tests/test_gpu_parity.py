@@ -1107,8 +1107,8 @@ def test_flat_stream_rollout_rates_vs_oracle(gpu, oracle, monkeypatch, family, l
         t += 1
 
 
-@pytest.mark.parametrize("mu_max,step_limit", [(9.0, 40), (14.0, 6), (40.0, 13), (60.0, 40), (100.0, 40),
-                                             (200.0, 5), (400.0, 40)])
+@pytest.mark.parametrize("mu_max,step_limit", [(9.0, 40), (14.0, 6), (40.0, 13), (60.0, 40), (70.0, 40),
+                                             (100.0, 40), (120.0, 17), (200.0, 5), (400.0, 40)])
 def test_newsvendor_rollout_sampler_mixes(gpu, monkeypatch, mu_max, step_limit):
     """nv_roll_kernel's two stream waves (PTRS / multiplication branch) under
     every mix of rates -- all envs on the multiplication method, mixed, all
