@@ -39,6 +39,24 @@ def kernel_avg_ns(csv_path, kern):
     return None
 
 
+def issue_frac(src, wl, mode, kern_ms):
+    """Newsvendor's issue-rate roofline from this round's SQ passes (bench.py
+    _issue): VALU + SALU wave-instructions per launch over 1 024 SIMDs x the
+    launch's cycles at 2.4 GHz / 2.2 cycles per instruction."""
+    if wl != "newsvendor" or mode not in ("step", "rollout"):
+        return " |"
+    sq = os.path.join(ROOT, "profiles", "_sq_tmp.json")
+    d = os.path.join(src, "sq_newsvendor")
+    if not os.path.isdir(d):
+        return " |"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "sq_summary.py"), d, sq], check=True,
+                   capture_output=True)
+    c = json.load(open(sq))[mode]["counters_mean_per_dispatch"]
+    os.remove(sq)
+    insts = c["SQ_INSTS_VALU"] + c["SQ_INSTS_SALU"]
+    return f" {insts / (1024 * kern_ms * 1e-3 * 2.4e9 / 2.2):.3f} |"
+
+
 def main():
     tag = sys.argv[1]
     rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
@@ -75,12 +93,17 @@ def main():
             r = b["roofline"]
             pmc = os.path.join(dst, f"pmc_{wl}.json" if mode == "step" else f"pmc_{wl}_{mode}.json")
             pm = json.load(open(pmc)) if os.path.exists(pmc) else {}
+            rp_ns = (pm.get("rocprof_kernel_ns_mean") if pm else None) or kernel_avg_ns(
+                os.path.join(dst, f"{wl}_{mode}_kernel_stats.csv"),
+                (KERNELS if mode == "step" else ROLL_KERNELS if mode == "rollout" else POL_KERNELS)[wl])
+            alg = r["bytes_per_env_step"] * b["config"]["envs_per_gpu"] * (1 if mode == "step" else 30)
             rows.append(f"| {wl} | {mode} | {b['config']['envs_per_gpu']} | {b['value'] / 1e9:.3f} G | "
                         f"{r['kernel_ms_mean'] * 1e3:.2f} | {r['bytes_per_env_step']:.0f} | {r['achieved']:.0f} | "
                         f"{r['frac']:.3f} | "
-                        + (f"{pm['rocprof_kernel_ns_mean'] / 1e3:.2f} | {pm['traffic_over_algorithmic']:.2f} |"
-                           if pm and pm.get('traffic_over_algorithmic') else
-                           f"{(kernel_avg_ns(os.path.join(dst, f'{wl}_{mode}_kernel_stats.csv'), (ROLL_KERNELS if mode == 'rollout' else POL_KERNELS)[wl]) or float('nan')) / 1e3:.2f} | |"))
+                        + (f"{rp_ns / 1e3:.2f} | {alg / rp_ns / 8000.0:.3f} | " if rp_ns else "| | ")
+                        + (f"{pm['traffic_over_algorithmic']:.2f} |" if pm and pm.get("traffic_over_algorithmic")
+                           else " |")
+                        + issue_frac(src, wl, mode, r["kernel_ms_mean"]))
     sq = os.path.join(src, "sq_newsvendor")
     if os.path.isdir(sq):
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "sq_summary.py"), sq,
@@ -92,8 +115,9 @@ def main():
     with open(os.path.join(dst, "SUMMARY.md"), "w") as f:
         f.write(f"# Round {rnd} measurements (gpurun_out/round_{tag}, 1x MI355X)\n\n")
         f.write("| workload | mode | envs | env-steps/s | kernel µs/launch (events) | B/env-step | "
-                "achieved GB/s | frac of 8 TB/s | rocprof µs/launch | PMC traffic / algorithmic |\n")
-        f.write("|---|---|---|---|---|---|---|---|---|---|\n")
+                "achieved GB/s | frac of 8 TB/s | rocprof µs/launch | frac on rocprof time | "
+                "PMC traffic / algorithmic | issue frac |\n")
+        f.write("|---|---|---|---|---|---|---|---|---|---|---|---|\n")
         f.write("\n".join(rows) + "\n")
     print(open(os.path.join(dst, "SUMMARY.md")).read())
 
