@@ -816,8 +816,9 @@ __device__ __forceinline__ void nv_chunk(int t, int rem, int step_limit, bool nx
 // roundings, comparisons and draw boundaries as numpy (a round's uniforms can
 // finish one draw and start the next) -- and the group's base state advances
 // by the uniforms actually consumed.  Owners (lanes with `own`) hand their
-// generator to the group and get it back advanced; the group's first lane
-// writes the draws into the owner's column of `dcol` ([CH][WAVE], as doubles:
+// generator to the group and get it back advanced; the lane holding a
+// draw-ending uniform writes that draw into the owner's column of `dcol`
+// ([CH][WAVE], as doubles:
 // the rollout's demand handoff rows hold every draw as a double, see nv_roll_kernel).
 // G = 16, 8 or 4 for up to 4, 8 or 16 envs; more than 16 envs (small mu_max)
 // keep the one-lane sequential sampler (the caller's fallback): returns false.
@@ -854,11 +855,10 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
     while (__ballot(j < nd)) {
         TTRIP_ADD(1);
         const bool live = j < nd;
-        uint64_t th, tl;
-        mul128(ah, al, s.hi, s.lo, th, tl);
-        const uint64_t lo = tl + sil;
-        th = th + sih + (lo < tl ? 1ULL : 0ULL);
-        tl = lo;
+        // state after jl + 1 LCG steps: A s + S inc (mod 2^128)
+        const unsigned __int128 nx = ((((unsigned __int128)s.hi) << 64) | s.lo) * ((((unsigned __int128)ah) << 64) | al) +
+                                     ((((unsigned __int128)sih) << 64) | sil);
+        const uint64_t th = (uint64_t)(nx >> 64), tl = (uint64_t)nx;
         const uint64_t x = th ^ tl;
         const unsigned rot = (unsigned)(th >> 58);
         const uint64_t o = (x >> rot) | (x << ((64u - rot) & 63u));
@@ -880,25 +880,33 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
                 stops |= cont ? 0u : (1u << (q0 + q));
             }
         }
-        int need = live ? nd - j : 0;
-        int used = G, last = -1;
-        while (__ballot(stops != 0 && need > 0)) {
-            if (stops != 0 && need > 0) {
-                const int pos = __builtin_ctz(stops);
-                if (jl == 0) dcol[j * WAVE + src] = (double)(last < 0 ? X + pos : pos - last - 1);
-                j++;
-                need--;
-                last = pos;
-                stops &= stops - 1;
-                if (need == 0) used = pos + 1;
-            }
+        // the draws, all at once: lane jl holds the round's stop at position jl
+        // (if there is one), its rank among the round's stops and the stop
+        // before it, so it writes that draw itself -- X + jl for the round's
+        // first stop, the gap to the previous one otherwise -- while it is
+        // among the `need` draws the chunk still wants
+        const int need = live ? nd - j : 0;
+        const uint32_t below = stops & ((1u << jl) - 1u);
+        const int idx = __popc(below);
+        const bool stop_here = ((stops >> jl) & 1u) != 0;
+        if (stop_here && idx < need) {
+            const int prev = below ? 31 - __builtin_clz(below) : -1;
+            dcol[(j + idx) * WAVE + src] = (double)(prev < 0 ? X + jl : jl - prev - 1);
         }
+        // the group's `need`-th stop, if this round reaches it: the uniforms
+        // after it stay in the stream (the next chunk starts at the one after)
+        const uint64_t fin = (uint64_t)__ballot(stop_here && idx == need - 1);
+        const uint32_t gfin = (uint32_t)(fin >> gbase) & (uint32_t)((1ull << G) - 1ull);
+        const int ns = __popc(stops);
+        const int used = gfin ? __builtin_ctz(gfin) + 1 : G;
         if (live) {
-            if (j == nd) {          // the chunk's draws are done: the next starts fresh
+            if (gfin) {             // the chunk's draws are done: the next starts fresh
+                j = nd;
                 X = 0;
                 prod = 1.0;
             } else {
-                X = last < 0 ? X + G : G - 1 - last;
+                j += ns;
+                X = ns == 0 ? X + G : G - 1 - (31 - __builtin_clz(stops));
             }
         }
         wave_lds_sync();
