@@ -933,10 +933,11 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
 //   wave 0 (PTRS stream)  draws the demands (newsvendor.py:146) of the envs whose
 //   wave 1 (mult stream)  rate takes numpy's PTRS branch (lam >= 10, or 0) /
 //                         multiplication branch (0 < lam < 10) for the next chunk
-//                         of launch steps into a double-buffered LDS ring, with
+//                         of launch steps into a three-chunk LDS ring, with
 //                         the episode's Poisson constants in registers.  A lane
 //                         works through its chunk's draws without waiting for
-//                         the other lanes' rejections (one flat loop).  The
+//                         the other lanes' rejections (one flat loop; a PTRS
+//                         lane done early runs ahead into the next chunk).  The
 //                         branch owning an env's generator runs its reset draws
 //                         (5 uniforms -> price, cost, h, k, mu, :100-123) and
 //                         hands params and generator state over in LDS; the
@@ -945,11 +946,12 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
 //                         its action is loaded a step ahead, before the previous
 //                         step's stores (vmcnt is in order).
 // A chunk carries at most one reset (its last step).  Handoff: the stream waves
-// fill buffer c & 1, barrier c, the dynamics wave consumes chunk c after
-// barrier c.  Same draws, same order, same arithmetic as nv_run_kernel.
+// fill buffer c % 3, barrier c, the dynamics wave consumes chunk c after
+// barrier c (the reset rows and the dynamics -> obs rows alternate over two
+// buffers).  Same draws, same order, same arithmetic as nv_run_kernel.
 template <int LT>
 #ifndef NV_ROLL_CH
-#define NV_ROLL_CH 8
+#define NV_ROLL_CH 6
 #endif
 struct NvRoll {
     static constexpr int CH = NV_ROLL_CH;
@@ -961,7 +963,7 @@ struct NvRoll {
     // hq [2][CH][WAVE] f32, the reward hr [2][CH][WAVE] f64, a reset's params
     // hp [2][5][WAVE] f32
     static constexpr size_t lds() {
-        return tile_bytes() + RHS_LDS_MAX * sizeof(double) + 2 * (size_t)CH * WAVE * sizeof(int64_t) +
+        return tile_bytes() + RHS_LDS_MAX * sizeof(double) + 3 * (size_t)CH * WAVE * sizeof(double) +
                2 * NP * (size_t)WAVE * sizeof(double) + (size_t)WAVE * sizeof(double) +
                4 * (JUMP_MAX + 1) * sizeof(uint64_t) + 2 * 2 * (size_t)WAVE * sizeof(uint64_t) +
                2 * (size_t)CH * WAVE * (sizeof(float) + sizeof(double)) + 2 * 5 * (size_t)WAVE * sizeof(float);
@@ -997,13 +999,13 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
     PtrsConst c = nv_rate_const(P.par[4 * S + el]);
     uint64_t *kw = kb + role * 2 * WAVE;   // this wave's task table: keys [WAVE], exp(-mu) bits [WAVE]
     bool reset_any = false;
-    int t = t_start, cb = 0;
+    int t = t_start, cb = 0, c3 = 0;
     for (int k0 = 0; k0 < K;) {
         int len;
         bool rs;
         nv_chunk(t, K - k0, P.step_limit, nxt, NvRoll<LT>::CH, len, rs);
         const int nd = len - (rs ? 1 : 0);                   // the reset step draws none
-        double *dcol = dbuf + cb * CH * WAVE;
+        double *dcol = dbuf + c3 * CH * WAVE;
         const uint64_t ph0 = P.cm.ph_step + (uint64_t)k0;    // launch step of the chunk's first step
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
         for (int j = role; j < nd; j += 2) dcol[j * WAVE + lane] = 20;
@@ -1079,6 +1081,7 @@ __device__ __forceinline__ void nv_stream_ph(const NvParams &P, int role, int la
         }
         k0 += len;
         cb ^= 1;
+        c3 = c3 == 2 ? 0 : c3 + 1;
     }
     nv_wg_sync();   // barrier nch: the obs wave's last chunk
     if (valid && reset_any && role == 0) {
@@ -1139,7 +1142,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     // double (numpy's k = (int64)kd), so the stream wave stores kd as it is and
     // the dynamics wave converts, off the PTRS wave's per-candidate path
     double *dbuf = lg_l + RHS_LDS_MAX;
-    double *pbuf = reinterpret_cast<double *>(dbuf + 2 * CH * WAVE);      // [2][NP][WAVE]
+    double *pbuf = reinterpret_cast<double *>(dbuf + 3 * CH * WAVE);      // [2][NP][WAVE]
     double *ubuf = pbuf + 2 * NP * WAVE;                                   // [WAVE] mult wave's uniforms
     uint64_t *jt = reinterpret_cast<uint64_t *>(ubuf + WAVE);              // [4][JUMP_MAX + 1] jump table
     uint64_t *kb = jt + 4 * (JUMP_MAX + 1);                                // [2][2][WAVE] fast stream: keys, rates
@@ -1181,7 +1184,8 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
         bool mine = nv_mult_branch(c.lam) == multw;
         if (!multw) ts.flush(lane);
         bool reset_any = false;
-        int t = t_start, cb = 0;
+        int t = t_start, cb = 0, c3 = 0;
+        int carry = 0;   // PTRS lanes: draws of this chunk already made during the previous one
         int ci = 0;
         (void)ci;
         TPROBE_W(1);
@@ -1190,7 +1194,8 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             bool rs;
             nv_chunk(t, K - k0, P.step_limit, nxt, CH, len, rs);
             const int nd = mine ? len - (rs ? 1 : 0) : 0;    // draws of this env (the reset step draws none)
-            double *db = dbuf + cb * CH * WAVE + lane;
+            const int c3n = c3 == 2 ? 0 : c3 + 1;
+            double *db = dbuf + c3 * CH * WAVE + lane;
 #if defined(INVSIM_ABL_ROLL_NO_DRAW)
             for (int j = 0; j < nd; j++) db[j * WAVE] = 20;
 #else
@@ -1207,14 +1212,31 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 if (c.lam == 0) {
                     for (int j = 0; j < nd; j++) db[j * WAVE] = 0;
                 } else {
-                    // numpy random_poisson_ptrs, one trial per iteration, lanes independent
+                    // numpy random_poisson_ptrs, one trial per iteration, lanes
+                    // independent.  Run-ahead: a lane done with this chunk goes on
+                    // with the next chunk's draws (into its ring buffer, which no
+                    // wave reads before barrier c + 1) while the others finish,
+                    // unless this chunk ends with a reset or is the launch's last;
+                    // the wave then pays the max over lanes of the whole launch's
+                    // trips, not the sum over chunks of each chunk's max.
+                    int nd2 = 0;
+                    if (!rs && k0 + len < K) {
+                        int len2;
+                        bool rs2;
+                        nv_chunk(t + len, K - k0 - len, P.step_limit, nxt, CH, len2, rs2);
+                        nd2 = mine ? len2 - (rs2 ? 1 : 0) : 0;
+                    }
+                    const int lim = nd + nd2;
+                    double *db2 = dbuf + c3n * CH * WAVE + lane - nd * WAVE;   // draw j >= nd -> next chunk's j - nd
 #ifdef INVSIM_TIMING
                     uint32_t trips = 0;
 #endif
-                    for (int j = 0; j < nd;) {
+                    int j = carry;
+                    while (__ballot(j < nd)) {
 #ifdef INVSIM_TIMING
                         trips++;
 #endif
+                        if (j >= lim) continue;
                         const double U = st.g.next_double() - 0.5;
                         const double V = st.g.next_double();
                         double kd;
@@ -1236,15 +1258,16 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                         }
 #endif
                         if (acc) {
-                            db[j * WAVE] = kd;
+                            (j < nd ? db : db2)[j * WAVE] = kd;
                             j++;
                         }
                     }
+                    carry = j - nd;
 #ifdef INVSIM_TIMING
                     TTRIP_ADD(wave_max_u32(trips));
 #endif
                 }
-            } else if (!nv_mult_chunk_grp(st.g, c.enlam, mine, len - (rs ? 1 : 0), dbuf + cb * CH * WAVE, ubuf, jt, lane)) {
+            } else if (!nv_mult_chunk_grp(st.g, c.enlam, mine, len - (rs ? 1 : 0), dbuf + c3 * CH * WAVE, ubuf, jt, lane)) {
                 // more than 16 envs on this branch: numpy random_poisson_mult, one
                 // uniform per iteration, lanes independent
                 int64_t X = 0;
@@ -1289,6 +1312,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             }
             k0 += len;
             cb ^= 1;
+            c3 = c3n;
         }
         nv_wg_sync();   // barrier nch: the obs wave's last chunk
         if (valid) {
@@ -1404,7 +1428,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
     double lvl = 0.0;     // CLASSIC_NV / SS: the episode's ppf level, once computed
     bool have = false;
     int64_t dlast = -1;   // the last step's demand (the info record), -1: a reset step
-    int kk = 0, cb = 0;
+    int kk = 0, cb = 0, c3 = 0;
     int ci = 0;
     (void)ci;
     nv_wg_sync();   // barrier 0: chunk 0 ready
@@ -1442,7 +1466,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
                 else act = pol.cf[0];
                 if (valid && pol.act_out) out_store((float *)pol.act_out + oi, act);
             }
-            const int64_t d = (int64_t)dbuf[(cb * CH + kk) * WAVE + lane];
+            const int64_t d = (int64_t)dbuf[(c3 * CH + kk) * WAVE + lane];
             double r;
             nv_step_regs<LT>(P, e, valid, sc, st, act, nullptr, lg_l, nullptr, r, nullptr, d,
                              (valid && k == K - 1) ? (double *)P.cm.info_rec : nullptr, false);
@@ -1463,6 +1487,7 @@ nv_roll_kernel(NvParams P, int t_start, StepIO<float, float> io, PolicyIO pol) {
             nv_wg_sync();                            // barrier of the next chunk (after the last: the obs wave's)
             kk = 0;
             cb ^= 1;
+            c3 = c3 == 2 ? 0 : c3 + 1;
         }
     }
     if (valid) {
