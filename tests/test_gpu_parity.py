@@ -814,6 +814,8 @@ def test_net_demand_wave_rollout_equals_one_wave(gpu, monkeypatch, graph, backlo
     (9, 40, 65536, 3, (45,), "next_step"),
     (16, 10, 777, 2, (30,), "next_step"),
     (5, 12, 1000, 5, (8, 17), "disabled"),       # stepping past step_limit
+    (5, 6, 2000, 0, (36, 7, 1, 13), "next_step"),  # episodes of one chunk: run-ahead stops at every reset
+    (3, 50, 3000, 4, (97, 5), "next_step"),      # long run-ahead chains, a launch ending mid-chunk
 ])
 def test_newsvendor_stream_wave_rollout_equals_one_wave(gpu, monkeypatch, L, step_limit, n, pre, Ks, mode):
     """invsim_rollout of Newsvendor runs nv_roll_kernel (stream wave drawing
