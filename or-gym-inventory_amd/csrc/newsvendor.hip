@@ -820,17 +820,22 @@ __device__ __forceinline__ void nv_chunk(int t, int rem, int step_limit, bool nx
 // draw-ending uniform writes that draw into the owner's column of `dcol`
 // ([CH][WAVE], as doubles:
 // the rollout's demand handoff rows hold every draw as a double, see nv_roll_kernel).
-// G = 16, 8 or 4 for up to 4, 8 or 16 envs; more than 16 envs (small mu_max)
-// keep the one-lane sequential sampler (the caller's fallback): returns false.
+// G = 16 for up to 4 envs, then the even count that fits (12 for 5 envs, ...,
+// 4 for 11-16); more than 16 envs (small mu_max) keep the one-lane sequential
+// sampler (the caller's fallback): returns false.
 __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own, int nd, double *dcol,
                                                   double *ubuf, const uint64_t *jt, int lane) {
     const uint64_t mm = (uint64_t)__ballot(own && nd > 0);
     const int nm = __popcll(mm);
     if (nm > 16) return false;
     if (nm == 0) return true;
-    const int lg = nm > 8 ? 2 : nm > 4 ? 3 : 4;          // log2 G
-    const int G = 1 << lg;
-    const int grp = lane >> lg, jl = lane & (G - 1), gbase = grp << lg;
+    // G: 16 lanes per env up to 4 envs, else the even count that fits (12,
+    // 10, 8, 8, 6, 6, then 4): the workgroups with 5-10 such envs are the
+    // kernel's tail, and their rounds scale with 1 / G
+    const int G = nm <= 4 ? 16 : nm == 5 ? 12 : nm == 6 ? 10 : nm <= 8 ? 8 : nm <= 10 ? 6 : 4;
+    // lane / G as a multiply and shift (exact for lanes < 64 with these G)
+    const int M = G == 16 ? 4096 : G == 12 ? 5462 : G == 10 ? 6554 : G == 8 ? 8192 : G == 6 ? 10923 : 16384;
+    const int grp = (lane * M) >> 16, jl = lane - grp * G, gbase = grp * G;
     const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
     int *slot = reinterpret_cast<int *>(ubuf);
@@ -865,15 +870,28 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
         ubuf[lane] = (double)(o >> 11) * (1.0 / 9007199254740992.0);
         wave_lds_sync();
         // the product chain over the round's uniforms in stream order (4 loaded
-        // at a time; G is a multiple of 4): prod, and a bit per uniform that
+        // at a time, then 2 when G is not a multiple of 4): prod, and a bit per uniform that
         // ends a draw (prod <= enlam); then the draws, in order, from the bits
         uint32_t stops = 0;
-        for (int q0 = 0; q0 < G; q0 += 4) {
+        int q0 = 0;
+        for (; q0 + 4 <= G; q0 += 4) {
             double u[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) u[q] = ubuf[gbase + q0 + q];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
+                const double pq = prod * u[q];
+                const bool cont = pq > en;
+                prod = cont ? pq : 1.0;
+                stops |= cont ? 0u : (1u << (q0 + q));
+            }
+        }
+        if (q0 < G) {           // G = 4 m + 2: the last two
+            double u[2];
+#pragma unroll
+            for (int q = 0; q < 2; q++) u[q] = ubuf[gbase + q0 + q];
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
                 const double pq = prod * u[q];
                 const bool cont = pq > en;
                 prod = cont ? pq : 1.0;
@@ -918,7 +936,7 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
         }
     }
     // the advanced generator back to its owner (group `rank` -> lane rank * G)
-    const int back = (own && nd > 0) ? (rank << lg) : lane;
+    const int back = (own && nd > 0) ? rank * G : lane;
     const uint64_t bh = shfl_u64(s.hi, back), bl = shfl_u64(s.lo, back);
     if (own && nd > 0) {
         g.hi = bh;
