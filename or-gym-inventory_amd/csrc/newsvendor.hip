@@ -818,8 +818,8 @@ __device__ __forceinline__ void nv_chunk(int t, int rem, int step_limit, bool nx
 // by the uniforms actually consumed.  Owners (lanes with `own`) hand their
 // generator to the group and get it back advanced; the lane holding a
 // draw-ending uniform writes that draw into the owner's column of `dcol`
-// ([CH][WAVE], as doubles:
-// the rollout's demand handoff rows hold every draw as a double, see nv_roll_kernel).
+// ([CH][WAVE], as doubles: the rollout's demand handoff rows hold every draw
+// as a double, see nv_roll_kernel).
 // G = 16 for up to 4 envs, then the even count that fits (12 for 5 envs, ...,
 // 4 for 11-16); more than 16 envs (small mu_max) keep the one-lane sequential
 // sampler (the caller's fallback): returns false.
