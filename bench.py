@@ -54,6 +54,20 @@ WORKLOADS = {
                         desc="NetInvMgmtBacklogEnv default topology, 32768 instances"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_ACHIEVABLE_GBS = 6300.0  # what a streaming kernel reaches (MI355X_MICROARCH.md, HBM section)
+# The reference's own CPU step, measured in the survey container (BASELINE.md
+# section 2: numpy/networkx, 8 independent processes on an 8-vCPU Intel Xeon KVM
+# guest, constant actions, aggregate env-steps/s).  The reference cannot run on
+# the GPU box, so this is quoted with its provenance, not re-timed.
+REFERENCE_PYTHON = {
+    "invmgmt_backlog": (200e3, "InvManagementBacklogEnv m=4"),
+    "invmgmt_lostsales": (204e3, "InvManagementLostSalesEnv m=4"),
+    "newsvendor": (561e3, "NewsvendorEnv L=5"),
+    "net_backlog": (722.0, "NetInvMgmtBacklogEnv default graph"),
+}
+# profiles/rNN round whose committed rocprof / PMC files the line quotes (None:
+# the newest round that has the file)
+PROFILE_ROUND = None
 
 
 def parse():
@@ -82,6 +96,9 @@ def parse():
                     help="step mode: skip the HIP-graph replay region reported under 'graph'")
     ap.add_argument("--no-rollout-line", action="store_true",
                     help="step mode: skip the K-step rollout region reported under 'rollout'")
+    ap.add_argument("--no-config-lines", action="store_true",
+                    help="default step run: skip the compact lines of the other BASELINE configs "
+                         "(Newsvendor, the LostSales shard, NetInvMgmt) reported under 'configs'")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--pool", type=int, default=16, help="distinct action batches cycled")
     ap.add_argument("--demand-stream", default="numpy", choices=["numpy", "philox"],
@@ -189,6 +206,21 @@ def _spawn_ranks(args):
 def _fold_rows(stats, rew, term, trunc, rows, sp):
     if rows:
         stats.update_block(rew[:rows], term[:rows], trunc[:rows], stream=sp)
+
+
+def _span(t0, t1, dev, dist):
+    """The timed region across ranks: from the earliest rank's start to the
+    latest rank's end.  time.perf_counter is CLOCK_MONOTONIC, one clock for
+    every process of the node, so the ranks' stamps compare directly; the span
+    includes the skew of the ranks' exits from the opening barrier (a max of
+    per-rank durations would drop it)."""
+    if not dist.is_initialized():
+        return t1 - t0
+    import torch
+    cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([-t0, t1], dtype=torch.float64, device=cdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[1].item()) + float(t[0].item())
 
 
 def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
@@ -337,17 +369,10 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
         t1 = time.perf_counter()
     # the closing barrier brackets the region on every rank; each rank's clock
     # stops when its own work is done (not after the barrier's latency, which
-    # is tens of us over RCCL against a ~0.2 ms driver-style region), and the
-    # max over ranks below is the last rank's finish
+    # is tens of us over RCCL against a ~0.2 ms driver-style region)
     if dist.is_initialized():
         dist.barrier()
-    el = t1 - t0
-    backend = dist.get_backend() if dist.is_initialized() else None
-    cdev = dev if backend == "nccl" else torch.device("cpu")
-    if dist.is_initialized():
-        t = torch.tensor([el], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = _span(t0, t1, dev, dist)
     ep = stats.allreduce()                                  # RCCL all-reduce of the timed batch's statistics
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / calls
     total_steps = calls * steps_per_call
@@ -425,12 +450,7 @@ def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
     torch.cuda.synchronize(dev)
     if dist.is_initialized():                 # bracket; each rank's clock stopped at its own end (above)
         dist.barrier()
-    el = t1 - t0
-    if dist.is_initialized():
-        cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
-        t = torch.tensor([el], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = _span(t0, t1, dev, dist)
     ep = stats.allreduce()
     total = reps * C
     return {"value": total * N * world / el, "unit": "env-steps/s", "steps": total, "replays": reps,
@@ -439,6 +459,22 @@ def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
             "cycles_per_replay": Q,
             "what": "invsim_step x Q (periods+1) + one episode fold per replay, one HIP graph (StepGraph)",
             "episode_stats": dict(ep, source="the replays' own episode fold, one all-reduce after the region")}
+
+
+def _hbm_counter(traffic, traffic_src, rocprof):
+    """The physical HBM rate of the dominant kernel: the PMC counter bytes per
+    launch (FETCH_SIZE x2 + WRITE_SIZE, calibrated, tools/pmc_summary.py) over
+    the same kernel's rocprofv3 mean duration, against the 8 TB/s peak and the
+    ~6.3 TB/s a streaming kernel achieves.  Both figures come from committed
+    profiles/rNN files of this workload and mode at this batch size."""
+    if not traffic or not rocprof:
+        return None
+    ach = traffic / rocprof["dominant_ns"]
+    return {"achieved": ach, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "frac_of_achievable": ach / HBM_ACHIEVABLE_GBS, "achievable": HBM_ACHIEVABLE_GBS,
+            "bytes_per_launch": traffic, "dominant_ns": rocprof["dominant_ns"],
+            "sources": [traffic_src, rocprof["source"]],
+            "what": "counter HBM bytes per launch / rocprofv3 mean duration of the dominant kernel"}
 
 
 def _roofline(r, traffic, traffic_src, rocprof=None, issue=None):
@@ -458,6 +494,9 @@ def _roofline(r, traffic, traffic_src, rocprof=None, issue=None):
     if rocprof:
         rocprof["event_over_all_launches"] = r["kern_ms"] * 1e6 / rocprof["all_step_launches_ns"]
         out["rocprof"] = rocprof
+    hc = _hbm_counter(traffic, traffic_src, rocprof)
+    if hc:
+        out["hbm_counter"] = hc
     if issue:
         out["issue"] = issue
     return out
@@ -472,7 +511,8 @@ _STEP_KERNELS = ("_split_kernel", "_step1_kernel", "_step2_kernel", "_run_kernel
 
 def _newest(pattern):
     import glob
-    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", pattern)))
+    rnd = PROFILE_ROUND or "r[0-9][0-9]"
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", rnd, pattern)))
     return fs[-1] if fs else None
 
 
@@ -503,15 +543,15 @@ def _rocprof(workload, mode, n_match, alg_bytes):
             "all_step_launches_ns": mean_all, "frac_all_launches": alg_bytes / mean_all / HBM_PEAK_GBS}
 
 
-def _issue(workload, mode, kern_ms):
+def _issue(workload, mode, kern_ms, n_match):
     """Issue-rate roofline of the Newsvendor kernels, whose bound is the
     instruction stream, not HBM: VALU + SALU wave-instructions per
     launch (SQ_INSTS_VALU + SQ_INSTS_SALU, newest profiles/rNN/sq_newsvendor.json)
     over what 1 024 SIMDs issue in the launch's duration at the measured best
     SIMD issue interval (v_add_u32 with four waves: 2.2 cycles,
     profiles/r04/launch/valu_rates.txt) at 2.4 GHz."""
-    if workload != "newsvendor" or mode not in ("step", "rollout"):
-        return None
+    if workload != "newsvendor" or mode not in ("step", "rollout") or not n_match:
+        return None          # the SQ passes ran the default batch with the numpy stream only
     f = _newest("sq_newsvendor.json")
     if not f:
         return None
@@ -531,13 +571,55 @@ def _issue(workload, mode, kern_ms):
 def _pmc(workload, mode, n_match):
     """The newest round's PMC summary for this workload and mode
     (profiles/rNN/pmc_<workload>[_rollout].json, tools/pmc_summary.py)."""
-    import glob
     suffix = {"step": "", "rollout": "_rollout", "policy": "_policy"}[mode]
-    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", f"pmc_{workload}{suffix}.json")))
-    if not pmcs or not n_match:
+    f = _newest(f"pmc_{workload}{suffix}.json")
+    if not f or not n_match:
         return None, None
-    rec = json.load(open(pmcs[-1]))
-    return rec["hbm_bytes_per_launch"], os.path.relpath(pmcs[-1], ROOT)
+    rec = json.load(open(f))
+    return rec["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+
+
+def config_line(args, name, world, rank, dev, dist):
+    """A compact line for another BASELINE config, timed in the same run the
+    same way as the headline (eager step region, then the fused K-step rollout
+    region): Newsvendor 65 536 (config 2), the per-GPU shard of InvMgmt
+    LostSales 262 144 over 8 GPUs (config 4: 32 768 envs, global offset
+    rank x 32 768) and NetInvMgmt Backlog 32 768 (config 5)."""
+    import torch
+    import invsim
+    wl = WORKLOADS[name]
+    n = wl["n"]
+    env = getattr(invsim, wl["cls"])(n, device=dev, global_offset=rank * n, copy=False)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(4321 + rank)
+    env.reset(seed=0)
+    r = run_region(args, env, wl, "step", args.steps, args.warmup, world, dev, gen, dist)
+    traffic, tsrc = _pmc(name, "step", True)
+    roof = _roofline(r, traffic, tsrc, _rocprof(name, "step", True, r["B"] * n), _issue(name, "step", r["kern_ms"], True))
+    C = env._horizon() + 1
+    Kr = args.rollout_k
+    unit = C * Kr
+    rr = run_region(args, env, wl, "rollout", unit * max(1, -(-args.steps // unit)), 2 * Kr, world, dev, gen, dist)
+    t2, s2 = _pmc(name, "rollout", True)
+    roof2 = _roofline(rr, t2, s2, _rocprof(name, "rollout", True, rr["B"] * n * rr["K"]),
+                      _issue(name, "rollout", rr["kern_ms"], True))
+
+    def compact(x, ro):
+        out = {"value": x["total_steps"] * n * world / x["el"], "ms_per_step": x["el"] * 1e3 / x["total_steps"],
+               "steps": x["total_steps"], "bytes_per_env_step": x["B"], "frac": ro["frac_kernel"],
+               "frac_wall": ro["frac_wall"]}
+        if "rocprof" in ro:
+            out["frac_rocprof"] = ro["rocprof"]["frac_dominant"]
+            out["dominant_kernel"] = ro["rocprof"]["dominant_kernel"]
+        if "hbm_counter" in ro:
+            out["hbm_counter"] = {k: ro["hbm_counter"][k] for k in ("achieved", "frac", "frac_of_achievable")}
+        if "issue" in ro:
+            out["issue_frac"] = ro["issue"]["frac"]
+        return out
+    line = {"workload": wl["desc"], "envs_per_gpu": n, "global_envs": n * world, "dtype": wl["dtype"],
+            "step": compact(r, roof), "rollout": dict(compact(rr, roof2), K=rr["K"])}
+    del env
+    return line
 
 
 def main():
@@ -610,7 +692,7 @@ def main():
                    "backend": (backend if dist.is_initialized() else None), "demand_stream": args.demand_stream},
         "roofline": _roofline(r, traffic, traffic_src,
                               _rocprof(args.workload, args.mode, full, r["B"] * N * r["steps_per_call"]),
-                              _issue(args.workload, args.mode, r["kern_ms"])),
+                              _issue(args.workload, args.mode, r["kern_ms"], full)),
         "episode_stats": dict(r["ep"], source="timed batch: HIP episode fold of the timed steps' rewards and "
                                               "done flags, one all-reduce after the region"),
     }
@@ -634,14 +716,26 @@ def main():
                           "ms_per_launch": rr["el"] * 1e3 / rr["calls"],
                           "roofline": _roofline(rr, t2, s2,
                                                 _rocprof(args.workload, "rollout", full, rr["B"] * N * rr["K"]),
-                                                _issue(args.workload, "rollout", rr["kern_ms"])),
+                                                _issue(args.workload, "rollout", rr["kern_ms"], full)),
                           "episode_stats": dict(rr["ep"], cycles=rr["total_steps"] // C,
                                                 source="timed rollout batch: HIP episode fold between "
                                                        "launch blocks, one all-reduce after the region")}
     if args.mode == "step" and not args.no_graph_line and args.demand_stream == "numpy":
         out["graph"] = run_graph_region(args, env, wl, args.steps, world, dev, gen, dist)
+    if (args.mode == "step" and args.workload == "invmgmt_backlog" and not args.n_envs and not args.strong
+            and args.demand_stream == "numpy" and not args.no_config_lines):
+        out["configs"] = {k: config_line(args, k, world, rank, dev, dist)
+                          for k in ("newsvendor", "invmgmt_lostsales", "net_backlog")}
+        out["configs"]["note"] = ("BASELINE configs 2, 4 (the per-GPU shard of 262 144 envs over 8 GPUs) and 5, "
+                                  "timed in this run like the headline: eager step region, then fused rollouts")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
+        rv, rwhat = REFERENCE_PYTHON[args.workload]
+        out["cpu_baseline"]["reference_python"] = {
+            "value": rv, "unit": "env-steps/s", "cores": 8,
+            "what": f"the reference's own {rwhat} step (numpy/networkx), 8 independent processes, constant actions",
+            "host": "Intel Xeon KVM guest, 8 vCPU (the survey container; the reference cannot run on the GPU box)",
+            "source": "BASELINE.md section 2 (measured, not re-timed here)"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

@@ -199,10 +199,12 @@ int common_fields(invsim_handle *h, Layout &lay, int64_t &o_rng, int64_t &o_peri
 
 // The A/B launch switches (kernels.hpp Knobs), read from the environment once,
 // here, when a handle is created: the only environment reads of the library.
+// A switch is "0" or "1" exactly; anything else (unset, empty, "false", "on")
+// keeps the default.
 bool env_flag(const char *name, bool dflt) {
     const char *v = std::getenv(name);
-    if (!v || !v[0]) return dflt;
-    return v[0] != '0';
+    if (!v || (v[0] != '0' && v[0] != '1') || v[1]) return dflt;
+    return v[0] == '1';
 }
 
 Knobs read_knobs() {
@@ -214,7 +216,11 @@ Knobs read_knobs() {
     k.im_ahead = env_flag("INVSIM_IM_AHEAD", k.im_ahead);
     if (const char *v = std::getenv("INVSIM_IM_ROLL3O_G2"); v && (v[0] == '0' || v[0] == '1'))
         k.im_roll3o_g2 = (int8_t)(v[0] - '0');
-    if (const char *v = std::getenv("INVSIM_IM_ROLL3O_MAX_N"); v && v[0]) k.im_roll3o_max_n = (int64_t)atoll(v);
+    if (const char *v = std::getenv("INVSIM_IM_ROLL3O_MAX_N"); v && v[0]) {   // a decimal count, else the default
+        char *end = nullptr;
+        const long long x = std::strtoll(v, &end, 10);
+        if (end && !*end && x >= 0) k.im_roll3o_max_n = (int64_t)x;
+    }
     k.nv_xcd = env_flag("INVSIM_NV_XCD", k.nv_xcd);
     k.nv_roll = env_flag("INVSIM_NV_ROLL", k.nv_roll);
     k.nv_pol_roll = env_flag("INVSIM_NV_POL_ROLL", k.nv_pol_roll);

@@ -857,6 +857,9 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
     int j = act ? 0 : nd;
     int X = 0;
     double prod = 1.0;
+    // the uniforms this lane's chain reads: its group's, or (idle lanes past the
+    // last group, need = 0) group 0's, so every read stays inside ubuf[WAVE]
+    const int rbase = act ? gbase : 0;
     while (__ballot(j < nd)) {
         TTRIP_ADD(1);
         const bool live = j < nd;
@@ -877,7 +880,7 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
         for (; q0 + 4 <= G; q0 += 4) {
             double u[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) u[q] = ubuf[gbase + q0 + q];
+            for (int q = 0; q < 4; q++) u[q] = ubuf[rbase + q0 + q];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const double pq = prod * u[q];
@@ -889,7 +892,7 @@ __device__ __forceinline__ bool nv_mult_chunk_grp(Pcg &g, double enlam, bool own
         if (q0 < G) {           // G = 4 m + 2: the last two
             double u[2];
 #pragma unroll
-            for (int q = 0; q < 2; q++) u[q] = ubuf[gbase + q0 + q];
+            for (int q = 0; q < 2; q++) u[q] = ubuf[rbase + q0 + q];
 #pragma unroll
             for (int q = 0; q < 2; q++) {
                 const double pq = prod * u[q];

@@ -54,20 +54,46 @@ def test_episode_stats_block_fold_host():
     assert res["episodes"] == acc[2] and res["reward_sum"] == pytest.approx(acc[3])
 
 
-def test_roofline_rocprof_reconciliation_fields():
+def test_roofline_rocprof_reconciliation_fields(monkeypatch):
     """the line's frac is reproduced from the committed
     rocprof kernel stats: the dominant kernel's mean and the mean over every
-    env-step launch (what the HIP-event figure averages), read from the newest
-    profiles/rNN/<workload>_<mode>_kernel_stats.csv."""
+    env-step launch (what the HIP-event figure averages).  Pinned to the
+    round-5 files: a later round's profiles do not move it."""
     import bench
+    monkeypatch.setattr(bench, "PROFILE_ROUND", "r05")
     alg = 746 * 65536
     r = bench._rocprof("invmgmt_backlog", "step", True, alg)
-    assert r is not None and r["source"].startswith("profiles/r")
+    assert r is not None and r["source"] == "profiles/r05/invmgmt_backlog_step_kernel_stats.csv"
     assert r["dominant_kernel"] == "im_split_kernel"
     assert 0.9 < r["dominant_share_of_launches"] < 1.0          # the reset launch every 31 steps
     assert r["all_step_launches_ns"] < r["dominant_ns"]            # the reset launch is cheaper
     assert abs(r["frac_dominant"] - alg / r["dominant_ns"] / 8000.0) < 1e-12
     assert bench._rocprof("invmgmt_backlog", "step", False, alg) is None   # another batch size: no file applies
-    i = bench._issue("newsvendor", "rollout", 0.06)
+    i = bench._issue("newsvendor", "rollout", 0.06, True)
     assert i["bound"] == "issue" and 0 < i["frac"] < 1 and i["instructions_per_launch"] > 1e6
-    assert bench._issue("invmgmt_backlog", "step", 0.009) is None
+    assert bench._issue("newsvendor", "rollout", 0.06, False) is None     # not the SQ passes' batch (ADVICE r05)
+    assert bench._issue("invmgmt_backlog", "step", 0.009, True) is None
+
+
+def test_hbm_counter_fraction(monkeypatch):
+    """the physical HBM rate = counter bytes per launch /
+    the dominant kernel's rocprof time; round 5's files give 4.53 TB/s (0.566)."""
+    import bench
+    monkeypatch.setattr(bench, "PROFILE_ROUND", "r05")
+    traffic, src = bench._pmc("invmgmt_backlog", "step", True)
+    rp = bench._rocprof("invmgmt_backlog", "step", True, 746 * 65536)
+    hc = bench._hbm_counter(traffic, src, rp)
+    assert hc["achieved"] == pytest.approx(41256485.86 / 9114.889764, rel=1e-6)
+    assert hc["frac"] == pytest.approx(0.566, abs=1e-3)
+    assert hc["frac_of_achievable"] == pytest.approx(hc["achieved"] / 6300.0)
+    assert bench._hbm_counter(None, None, rp) is None and bench._hbm_counter(traffic, src, None) is None
+
+
+def test_span_single_process():
+    import bench
+
+    class NoDist:
+        @staticmethod
+        def is_initialized():
+            return False
+    assert bench._span(1.0, 3.5, None, NoDist) == 2.5

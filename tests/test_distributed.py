@@ -85,3 +85,25 @@ def test_gloo_world2_shards_and_stats(tmp_path, oracle):
         assert st[0] == n_global
         assert st[1] == pytest.approx(ret.sum(), rel=1e-12)
         assert st[2] == pytest.approx((ret * ret).sum(), rel=1e-12)
+
+
+def _span_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank r started at 10 + r and ended at 20 - 3 r: the span is from the
+    # earliest start (10) to the latest end (20), not the longest duration (10)
+    el = bench._span(10.0 + rank, 20.0 - 3 * rank, torch.device("cpu"), dist)
+    np.save(os.path.join(out_dir, f"span_{rank}.npy"), np.array([el]))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_span(tmp_path):
+    """bench.py's multi-rank clock: earliest start to latest end
+    over the ranks, on the node's shared monotonic clock."""
+    mp.spawn(_span_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert np.load(tmp_path / f"span_{r}.npy")[0] == 10.0

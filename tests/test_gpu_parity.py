@@ -1344,3 +1344,49 @@ def test_net_lambda_receiver_is_checked_at_reset(gpu):
     view.step(np.full(view.action_space.shape, 5.0, np.float32))
     env.close()
     view.close()
+
+
+def test_config4_shard_at_nonzero_offset_vs_oracle(gpu, oracle):
+    """BASELINE config 4's rank-7 shard (InvManagementLostSalesEnv, 262 144
+    envs over 8 GPUs -> envs 7 x 32 768 .. 8 x 32 768 - 1) against the C oracle
+    seeded with those global indices (inventory_management.py:436-451; seed
+    s + global index, the SyncVectorEnv rule): single steps, then a fused
+    rollout across one NEXT_STEP reset, then single steps again -- bit-exact
+    obs, rewards and flags."""
+    import invsim
+    n, off, s0 = 32768, 7 * 32768, 77
+    oracle.set_threads(8)
+    try:
+        env = invsim.InvManagementLostSalesEnv(n, device=gpu, global_offset=off, record_demand=True)
+        orc = oracle.OracleInvMgmt(n, backlog=False)
+        orc.seed(range(s0 + off, s0 + off + n))
+        e_obs = orc.reset()
+        obs, _ = env.reset(seed=s0)
+        assert np.array_equal(obs.cpu().numpy(), e_obs)
+        rng = np.random.default_rng(17)
+        acts = np.stack([_im_random_actions(rng, n, 3, [100, 200, 230]) for _ in range(75)])
+        dev_acts = torch.from_numpy(acts).to(gpu)
+        outs = []
+        for k in range(20):                                  # steps 0..19
+            o, r, _, tr, _ = env.step(dev_acts[k])
+            outs.append((o.cpu().numpy(), r.cpu().numpy(), tr.cpu().numpy()))
+        o, r, _, tr = env.rollout(dev_acts[20:50])           # periods 20..29, the reset step, 0..18
+        outs += [(o[k].cpu().numpy(), r[k].cpu().numpy(), tr[k].cpu().numpy()) for k in range(30)]
+        for k in range(50, 75):                              # periods 19..29, reset, 0..12
+            o, r, _, tr, _ = env.step(dev_acts[k])
+            outs.append((o.cpu().numpy(), r.cpu().numpy(), tr.cpu().numpy()))
+        t = 0
+        for k, (go, gr, gt) in enumerate(outs):
+            if t >= 30:
+                assert np.array_equal(go, orc.reset()), k
+                assert (gr == 0).all() and not gt.any(), k
+                t = 0
+                continue
+            e_obs, e_rew, e_tr = orc.step(acts[k])
+            assert np.array_equal(go, e_obs), f"obs step {k}"
+            _assert_reward(gr, e_rew, f"step {k}")
+            assert np.array_equal(gt, e_tr), k
+            t += 1
+        assert t == 13
+    finally:
+        oracle.set_threads(1)
