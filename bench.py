@@ -84,10 +84,12 @@ def parse():
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: the workload's env count is the GLOBAL batch, split over ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--fold", default="inline", choices=["side", "inline", "none"],
-                    help="episodic-return fold of the timed outputs: between blocks on the kernel stream "
-                         "(default), on a side stream (measured slower: it shares the CUs with the step "
-                         "kernels), or off (A/B only: no episode_stats)")
+    ap.add_argument("--fold", default="auto", choices=["auto", "sink", "side", "inline", "none"],
+                    help="episodic-return statistics of the timed steps: sink = folded inside the step / "
+                         "rollout kernels (invsim_set_episode_sink; auto picks it for InvMgmt, whose "
+                         "kernels fold in-kernel), inline = a fold launch between blocks on the kernel "
+                         "stream (auto for the other families), side = that fold on a side stream "
+                         "(measured slower), none = off (A/B only: no episode_stats)")
     ap.add_argument("--stop", default="event", choices=["event", "sync"],
                     help="end of the timed region: the kernel stream's last event completing (default), or "
                          "torch.cuda.synchronize returning; the region is closed by torch.cuda.synchronize "
@@ -208,6 +210,16 @@ def _fold_rows(stats, rew, term, trunc, rows, sp):
         stats.update_block(rew[:rows], term[:rows], trunc[:rows], stream=sp)
 
 
+def fold_mode(args, env):
+    """--fold auto: the in-kernel episode sink where the family's step and
+    rollout kernels fold in-kernel (InvMgmt), else the fold launch between
+    blocks (the library would otherwise fold each launch's rows separately)."""
+    import invsim
+    if args.fold != "auto":
+        return args.fold
+    return "sink" if env.family == invsim._capi.INVSIM_INVMGMT else "inline"
+
+
 def _span(t0, t1, dev, dist):
     """The timed region across ranks: from the earliest rank's start to the
     latest rank's end.  time.perf_counter is CLOCK_MONOTONIC, one clock for
@@ -262,6 +274,9 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     po = obs.data_ptr()
     slab_ptrs = [(rew[b].data_ptr(), term[b].data_ptr(), trunc[b].data_ptr()) for b in range(2)]
     stats = EpisodeStats(N, dev)
+    fm = fold_mode(args, env)
+    if fm == "sink":           # the step / rollout kernels fold their rows into `stats` themselves
+        stats.attach(env)
     fstream = torch.cuda.Stream(dev)
     fsp = fstream.cuda_stream
     ev_out = [torch.cuda.Event() for _ in range(2)]     # slab written (kernel stream)
@@ -328,7 +343,7 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
         for bi in range(0, n_calls, calls_per_block):
             nb = min(calls_per_block, n_calls - bi)
             sl = blk[0] & 1
-            if args.fold == "side":
+            if fm == "side":
                 stream.wait_event(ev_free[sl])          # this slab's previous fold is done
             if timed:
                 evs[bi // calls_per_block][0].record(stream)
@@ -337,12 +352,12 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
             if timed:
                 evs[bi // calls_per_block][1].record(stream)
             rows = nb * rows_per_call
-            if args.fold == "side":
+            if fm == "side":
                 ev_out[sl].record(stream)
                 fstream.wait_event(ev_out[sl])
                 _fold_rows(stats, rew[sl], term[sl], trunc[sl], rows, fsp)
                 ev_free[sl].record(fstream)
-            elif args.fold == "inline":
+            elif fm == "inline":
                 _fold_rows(stats, rew[sl], term[sl], trunc[sl], rows, sp)
             blk[0] += 1
 
@@ -358,7 +373,7 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
         # the end of the work is `stream`'s last event completing
         # (hipEventSynchronize, no device-wide drain); with --fold side the last
         # block's fold runs on fstream, so `stream` waits for it first
-        if args.fold == "side":
+        if fm == "side":
             stream.wait_stream(fstream)
         end_ev.record(stream)
         end_ev.synchronize()
@@ -374,6 +389,8 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
         dist.barrier()
     el = _span(t0, t1, dev, dist)
     ep = stats.allreduce()                                  # RCCL all-reduce of the timed batch's statistics
+    ep["fold"] = fm
+    stats.detach()
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / calls
     total_steps = calls * steps_per_call
     # the fast stream reads an 8-B key instead of the 32-B PCG64 state and writes no state back
@@ -418,6 +435,9 @@ def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
     trunc = torch.empty((C, N), dtype=torch.bool, device=dev)
     obs = torch.empty((N, O), dtype=env.obs_dtype, device=dev)
     stats = EpisodeStats(N, dev)
+    sink = fold_mode(args, env) == "sink"
+    if sink:                    # the captured step kernels fold into `stats` themselves
+        stats.attach(env)
 
     def cycle():
         sp = torch._C._cuda_getCurrentRawStream(dev.index)
@@ -426,7 +446,8 @@ def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
                                  term[i].data_ptr(), trunc[i].data_ptr(), None, sp)
             if rc:
                 raise RuntimeError(invsim._capi.last_error(h))
-        stats.update_block(rew, term, trunc, stream=sp)
+        if not sink:
+            stats.update_block(rew, term, trunc, stream=sp)
     g = StepGraph(env, cycle, warmup=1)
     reps = max(1, -(-steps // C))
     stream = torch.cuda.current_stream(dev)
@@ -452,13 +473,16 @@ def run_graph_region(args, env, wl, steps, world, dev, gen, dist):
         dist.barrier()
     el = _span(t0, t1, dev, dist)
     ep = stats.allreduce()
+    stats.detach()
     total = reps * C
     return {"value": total * N * world / el, "unit": "env-steps/s", "steps": total, "replays": reps,
             "steps_per_replay": C, "ms_per_step": el * 1e3 / total,
             "event_ms_per_step": e0.elapsed_time(e1) / total,
             "cycles_per_replay": Q,
-            "what": "invsim_step x Q (periods+1) + one episode fold per replay, one HIP graph (StepGraph)",
-            "episode_stats": dict(ep, source="the replays' own episode fold, one all-reduce after the region")}
+            "what": "invsim_step x Q (periods+1), with the episode sink in the step kernels or one episode fold "
+                    "per replay, one HIP graph (StepGraph)",
+            "episode_stats": dict(ep, fold="sink" if sink else "inline",
+                                  source="the replays' own episode statistics, one all-reduce after the region")}
 
 
 def _hbm_counter(traffic, traffic_src, rocprof):
@@ -693,8 +717,9 @@ def main():
         "roofline": _roofline(r, traffic, traffic_src,
                               _rocprof(args.workload, args.mode, full, r["B"] * N * r["steps_per_call"]),
                               _issue(args.workload, args.mode, r["kern_ms"], full)),
-        "episode_stats": dict(r["ep"], source="timed batch: HIP episode fold of the timed steps' rewards and "
-                                              "done flags, one all-reduce after the region"),
+        "episode_stats": dict(r["ep"], source="timed batch: the episode sink in the step kernels (fold 'sink') or "
+                                              "the HIP episode fold of the timed steps' outputs (fold 'inline'), "
+                                              "one all-reduce after the region"),
     }
     C = env._horizon() + 1                                  # steps per episode cycle (NEXT_STEP)
     if r["total_steps"] < C:
@@ -718,8 +743,9 @@ def main():
                                                 _rocprof(args.workload, "rollout", full, rr["B"] * N * rr["K"]),
                                                 _issue(args.workload, "rollout", rr["kern_ms"], full)),
                           "episode_stats": dict(rr["ep"], cycles=rr["total_steps"] // C,
-                                                source="timed rollout batch: HIP episode fold between "
-                                                       "launch blocks, one all-reduce after the region")}
+                                                source="timed rollout batch: the episode sink in the rollout "
+                                                       "kernels, or the HIP episode fold between launch "
+                                                       "blocks; one all-reduce after the region")}
     if args.mode == "step" and not args.no_graph_line and args.demand_stream == "numpy":
         out["graph"] = run_graph_region(args, env, wl, args.steps, world, dev, gen, dist)
     if (args.mode == "step" and args.workload == "invmgmt_backlog" and not args.n_envs and not args.strong

@@ -48,8 +48,9 @@
 extern "C" {
 #endif
 
-#define INVSIM_ABI_VERSION 3   /* 2: market samplers appended to invsim_netinvmgmt_spec
-                                  3: graph capture (invsim_capture_begin / _end, invsim_position) */
+#define INVSIM_ABI_VERSION 4   /* 2: market samplers appended to invsim_netinvmgmt_spec
+                                  3: graph capture (invsim_capture_begin / _end, invsim_position)
+                                  4: episode sink (invsim_set_episode_sink, invsim_episode_fold_groups) */
 
 #define INVSIM_OK 0
 #define INVSIM_EINVAL (-22)
@@ -252,6 +253,27 @@ int invsim_rollout_policy(invsim_handle *h, int32_t K, const invsim_policy *poli
  * invsim.distributed.EpisodeStats all-reduces acc over RCCL. */
 int invsim_episode_fold(const double *reward, const uint8_t *terminated, const uint8_t *truncated, int32_t K,
                         int64_t n_envs, double *ret, double *acc, void *stream);
+
+/* The same fold into per-group partials, deterministic (no atomics): part
+ * [ceil(n_envs / 64)][4] f64 (+=), row g = [sum of finished-episode returns,
+ * sum of their squares, finished episodes, sum of every reward folded] of envs
+ * 64 g .. 64 g + 63.  Per env, in row order: ret += reward; at terminated |
+ * truncated the return is folded and restarts at 0; each group's per-lane sums
+ * over the K rows are then reduced by one xor butterfly and added to part[g].
+ * The statistics are the column sums of part. */
+int invsim_episode_fold_groups(const double *reward, const uint8_t *terminated, const uint8_t *truncated,
+                               int32_t K, int64_t n_envs, double *ret, double *part, void *stream);
+
+/* Episode sink: the evaluation harness's `episode_reward += reward` per step
+ * and its per-episode bookkeeping at done (benchmark_InvManagementBacklogEnv.py:
+ * 371, 386, 434), kept on the device inside the step.  With a sink set, every
+ * invsim_step / invsim_rollout / invsim_rollout_policy on h folds the rows it
+ * produces into ret [N] and part [ceil(N / 64)][4] exactly as
+ * invsim_episode_fold_groups over those rows would (same ret and part bits):
+ * the lock-step InvMgmt step and rollout kernels in-kernel, other launches by
+ * that fold of their outputs on the same stream (reward / terminated /
+ * truncated must then be given).  NULL, NULL detaches.  Not during capture. */
+int invsim_set_episode_sink(invsim_handle *h, double *ret, double *part);
 
 /* Debug builds only (make -C csrc ptrs_stats -> invsim/_lib/debug/): PTRS
  * log-acceptance statistics since the last clear, summed over kernels:

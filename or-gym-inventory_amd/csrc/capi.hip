@@ -936,6 +936,11 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         int rc = ph_counter_sync(h, s);
         if (rc != INVSIM_OK) return rc;
     }
+    // episode sink: a kernel that does not fold in-kernel leaves it to the
+    // group fold of its output rows below (the same arithmetic, kernels.hpp EpSink)
+    if (h->cm.ep_ret && h->N && !reward)
+        return fail(h, INVSIM_EINVAL, "the episode sink folds the reward outputs: pass reward / terminated / truncated");
+    bool sunk = false;
     hipError_t e = hipSuccess;
     switch (h->family) {
         case INVSIM_NEWSVENDOR: {
@@ -946,7 +951,7 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
         case INVSIM_INVMGMT: {
             StepIO<int64_t, int64_t> io{K, (const int64_t *)actions, (int64_t *)obs, reward, terminated, truncated,
                                         (int64_t *)final_obs};
-            e = im_run_launch(h->im, h->im_m1, h->im_backlog, t_u, pol, io, h->la_valid, h->la_slot, s);
+            e = im_run_launch(h->im, h->im_m1, h->im_backlog, t_u, pol, io, h->la_valid, h->la_slot, sunk, s);
             break;
         }
         case INVSIM_NETINVMGMT: {
@@ -960,6 +965,11 @@ static int run_steps(invsim_handle *h, int K, const void *actions, void *obs, do
     if (e != hipSuccess) {
         h->la_valid = false;
         return hip_fail(h, e, "step launch");
+    }
+    if (h->cm.ep_ret && !sunk) {
+        if (!reward) return fail(h, INVSIM_EINVAL, "the episode sink needs this launch's reward outputs");
+        e = episode_fold_groups_launch(reward, terminated, truncated, K, h->N, h->cm.ep_ret, h->cm.ep_part, s);
+        if (e != hipSuccess) return hip_fail(h, e, "episode sink fold");
     }
     if (h->demand_stream == INVSIM_DEMAND_PHILOX) h->ph_step += (uint64_t)K;   // one counter value per launch step
     if (h->t_known) {
@@ -1082,6 +1092,25 @@ int invsim_episode_fold(const double *reward, const uint8_t *terminated, const u
         return fail(nullptr, INVSIM_EINVAL, "episode_fold: null buffer or negative size");
     hipError_t e = episode_fold_launch(reward, terminated, truncated, K, n_envs, ret, acc, (hipStream_t)stream);
     return e == hipSuccess ? INVSIM_OK : hip_fail(nullptr, e, "episode_fold launch");
+}
+
+int invsim_episode_fold_groups(const double *reward, const uint8_t *terminated, const uint8_t *truncated,
+                               int32_t K, int64_t n_envs, double *ret, double *part, void *stream) {
+    TraceRange tr_("invsim_episode_fold_groups");
+    if ((!reward && K > 0 && n_envs > 0) || !ret || !part || K < 0 || n_envs < 0)
+        return fail(nullptr, INVSIM_EINVAL, "episode_fold_groups: null buffer or negative size");
+    hipError_t e = episode_fold_groups_launch(reward, terminated, truncated, K, n_envs, ret, part, (hipStream_t)stream);
+    return e == hipSuccess ? INVSIM_OK : hip_fail(nullptr, e, "episode_fold_groups launch");
+}
+
+int invsim_set_episode_sink(invsim_handle *h, double *ret, double *part) {
+    if (!h) return fail(nullptr, INVSIM_EINVAL, "null handle");
+    if (int rc = refuse_in_capture(h, "set_episode_sink")) return rc;
+    if ((ret == nullptr) != (part == nullptr)) return fail(h, INVSIM_EINVAL, "episode sink: ret and part together");
+    h->cm.ep_ret = ret;
+    h->cm.ep_part = part;
+    sync_common(h);
+    return INVSIM_OK;
 }
 
 int invsim_debug_ptrs_stats(uint64_t *out, int32_t clear) {

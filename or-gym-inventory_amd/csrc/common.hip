@@ -110,7 +110,57 @@ episode_fold_kernel(const double *rew, const uint8_t *term, const uint8_t *trunc
     }
 }
 
+// The episode sink's fold (kernels.hpp EpLane / EpPart) of K output rows: one
+// wave per 64-env group g, lane e walks its rows in step order (loads issued in
+// blocks of FB, as above), then the wave's butterfly and lane 0's update of
+// part[g].  The fused step / rollout kernels run the same per-lane code on the
+// rows they produce, so both give the same ret and part bits.
+__global__ void __launch_bounds__(256)
+episode_fold_groups_kernel(const double *rew, const uint8_t *term, const uint8_t *trunc, int32_t K, int64_t N,
+                           double *ret, double *part) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t e = g * 64 + lane;
+    if (g * 64 >= N) return;                      // wave-uniform: a whole group past the batch
+    EpPart pp;
+    pp.load(part + 4 * g);
+    EpLane a;
+    bool any_done = false;
+    if (e < N) {
+        a.r = ret[e];
+        constexpr int FB = 16;
+        for (int k0 = 0; k0 < K; k0 += FB) {
+            double x[FB];
+            uint8_t d[FB];
+#pragma unroll
+            for (int u = 0; u < FB; ++u) {
+                const int64_t i = (int64_t)min(k0 + u, K - 1) * N + e;
+                x[u] = __builtin_nontemporal_load(rew + i);
+                d[u] = (uint8_t)((term ? __builtin_nontemporal_load(term + i) : 0) |
+                                 (trunc ? __builtin_nontemporal_load(trunc + i) : 0));
+            }
+#pragma unroll
+            for (int u = 0; u < FB; ++u) {
+                if (k0 + u < K) {
+                    a.add(x[u], d[u] != 0);
+                    any_done |= d[u] != 0;
+                }
+            }
+        }
+        ret[e] = a.r;
+    }
+    pp.flush(part + 4 * g, a, __ballot(any_done) != 0, lane);
+}
+
 static inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t episode_fold_groups_launch(const double *rew, const uint8_t *term, const uint8_t *trunc, int32_t K,
+                                      int64_t N, double *ret, double *part, hipStream_t s) {
+    if (N == 0 || K == 0) return hipSuccess;
+    hipLaunchKernelGGL(episode_fold_groups_kernel, dim3(grid_for(N, 256)), dim3(256), 0, s, rew, term, trunc, K, N,
+                       ret, part);
+    return hipGetLastError();
+}
 
 hipError_t episode_fold_launch(const double *rew, const uint8_t *term, const uint8_t *trunc, int32_t K,
                                int64_t N, double *ret, double *acc, hipStream_t s) {

@@ -813,6 +813,15 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
     TPROBE_AT(3, WAVE);
     const double apow = P.alpha_pow[t];
     const int64_t *arow = io.act + (valid ? e : N - 1) * M1;
+    // episode sink (kernels.hpp EpSink): the running return and the group's
+    // partials are loaded with the step's other loads
+    double *const ep_part = P.cm.ep_ret ? P.cm.ep_part + 4 * (e0 / WAVE) : nullptr;
+    EpPart epp;
+    double ep_r = 0.0;
+    if (ep_part) {
+        epp.load(ep_part);
+        ep_r = P.cm.ep_ret[valid ? e : N - 1];
+    }
     int64_t req[M1], arr[M1], I[M1], B[M1 + 1];
 #pragma unroll
     for (int i = 0; i < M1; i++) req[i] = arow[i];
@@ -878,45 +887,55 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
             store_tile<(M1 * 11 * WAVE * 8 / 2 + 16 * WAVE - 1) / (16 * WAVE)>(im_tile + h, io.obs + e0 * O + h,
                                                                               tcount - h, lane);
     }
-    if (!valid) return;
-    if (P.cm.info_rec) {   // step info (:334-345), as im_step_regs
-        constexpr int W = 2 * (M1 + 1) + 5;
-        int64_t *rr = (int64_t *)P.cm.info_rec + e * W;
+    if (valid) {
+        if (P.cm.info_rec) {   // step info (:334-345), as im_step_regs
+            constexpr int W = 2 * (M1 + 1) + 5;
+            int64_t *rr = (int64_t *)P.cm.info_rec + e * W;
 #pragma unroll
-        for (int q = 0; q <= M1; q++) {
-            rr[q] = Sv[q];
-            rr[M1 + 1 + q] = U[q];
+            for (int q = 0; q <= M1; q++) {
+                rr[q] = Sv[q];
+                rr[M1 + 1 + q] = U[q];
+            }
+            const double rev = np_sum<double>(M1 + 1, [&](int q) { return P.up[q] * (double)Sv[q]; });
+            const double pro = np_sum<double>(M1 + 1, [&](int q) { return P.uc[q] * (double)Sv[q]; });
+            const double hol = np_sum<double>(M1 + 1, [&](int q) {
+                const int64_t inv = (q < M1) ? Icur[q] : 0;
+                return P.hc[q] * (double)(inv > 0 ? inv : 0);
+            });
+            const double pen = np_sum<double>(M1 + 1, [&](int q) { return P.kc[q] * (double)U[q]; });
+            rr[2 * (M1 + 1) + 0] = __double_as_longlong(profit);
+            rr[2 * (M1 + 1) + 1] = __double_as_longlong(rev);
+            rr[2 * (M1 + 1) + 2] = __double_as_longlong(pro);
+            rr[2 * (M1 + 1) + 3] = __double_as_longlong(hol);
+            rr[2 * (M1 + 1) + 4] = __double_as_longlong(pen);
         }
-        const double rev = np_sum<double>(M1 + 1, [&](int q) { return P.up[q] * (double)Sv[q]; });
-        const double pro = np_sum<double>(M1 + 1, [&](int q) { return P.uc[q] * (double)Sv[q]; });
-        const double hol = np_sum<double>(M1 + 1, [&](int q) {
-            const int64_t inv = (q < M1) ? Icur[q] : 0;
-            return P.hc[q] * (double)(inv > 0 ? inv : 0);
-        });
-        const double pen = np_sum<double>(M1 + 1, [&](int q) { return P.kc[q] * (double)U[q]; });
-        rr[2 * (M1 + 1) + 0] = __double_as_longlong(profit);
-        rr[2 * (M1 + 1) + 1] = __double_as_longlong(rev);
-        rr[2 * (M1 + 1) + 2] = __double_as_longlong(pro);
-        rr[2 * (M1 + 1) + 3] = __double_as_longlong(hol);
-        rr[2 * (M1 + 1) + 4] = __double_as_longlong(pen);
+        ImPending<M1> pend;
+#pragma unroll
+        for (int i = 0; i < M1; i++) {
+            pend.R[i] = R[i];                                           // ring slot t mod L <- R[t] (:267)
+            pend.req[i] = req[i];                                       // action_log[t] (:268)
+        }
+        pend.t = t;
+        im_flush_pending<M1>(P, pend, e);
+        out_store(io.rew + e, reward);
+        out_store(io.term + e, (uint8_t)0);
+        out_store(io.trunc + e, (uint8_t)(t1 >= P.periods ? 1 : 0));   // :350
+        if (P.cm.info_demand) P.cm.info_demand[e] = d;
+#pragma unroll
+        for (int i = 0; i < M1; i++) st_store(P.I + i * S + e, Icur[i]);   // :326
+        if (BACKLOG) {
+#pragma unroll
+            for (int q = 0; q <= M1; q++) st_store(P.B + q * S + e, U[q]);   // :307-312
+        }
     }
-    ImPending<M1> pend;
-#pragma unroll
-    for (int i = 0; i < M1; i++) {
-        pend.R[i] = R[i];                                           // ring slot t mod L <- R[t] (:267)
-        pend.req[i] = req[i];                                       // action_log[t] (:268)
-    }
-    pend.t = t;
-    im_flush_pending<M1>(P, pend, e);
-    out_store(io.rew + e, reward);
-    out_store(io.term + e, (uint8_t)0);
-    out_store(io.trunc + e, (uint8_t)(t1 >= P.periods ? 1 : 0));   // :350
-    if (P.cm.info_demand) P.cm.info_demand[e] = d;
-#pragma unroll
-    for (int i = 0; i < M1; i++) st_store(P.I + i * S + e, Icur[i]);   // :326
-    if (BACKLOG) {
-#pragma unroll
-        for (int q = 0; q <= M1; q++) st_store(P.B + q * S + e, U[q]);   // :307-312
+    if (ep_part) {   // after the stores: the butterfly runs while they drain
+        EpLane a;
+        if (valid) {
+            a.r = ep_r;
+            a.add(reward, t1 >= P.periods);               // terminated is always False (:350)
+            P.cm.ep_ret[e] = a.r;
+        }
+        epp.flush(ep_part, a, t1 >= P.periods, lane);
     }
     TWAIT();
     TPROBE_AT(4, WAVE);   // the dynamics wave's exit (probe 3: its entry)
@@ -1113,6 +1132,15 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO p
     double napow = P.alpha_pow[t < P.periods ? t : 0];   // alpha**t of the next step, prefetched
     int64_t dlast = 0;
     bool last_real = false;
+    // episode sink (kernels.hpp EpSink), accumulated in registers over the launch
+    double *const ep_part = P.cm.ep_ret ? P.cm.ep_part + 4 * (e0 / WAVE) : nullptr;
+    EpPart epp;
+    EpLane ep;
+    bool ep_done = false;
+    if (ep_part) {
+        epp.load(ep_part);
+        ep.r = valid ? P.cm.ep_ret[e] : 0.0;
+    }
     wg_lds_sync();   // barrier 0: chunk 0 ready
     for (int c = 0; c < nch; c++) {
         const int64_t *db = dbuf + (c % G::RD) * CH * WAVE;
@@ -1143,6 +1171,7 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO p
                     out_store(io.term + oi, (uint8_t)0);
                     out_store(io.trunc + oi, (uint8_t)0);
                 }
+                if (ep_part) ep.add(0.0, false);   // the reset step's row: reward 0, no flag
                 t = 0;
             } else {
                 const int64_t d = db[kk * WAVE + lane];
@@ -1259,6 +1288,11 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO p
                         out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.periods ? 1 : 0));   // :350
                     }
                 }
+                if (ep_part) {
+                    const bool done = valid && t + 1 >= P.periods;
+                    ep.add(valid ? reward : 0.0, done);
+                    ep_done |= done;
+                }
                 // age the windows by one period
 #pragma unroll
                 for (int i = 0; i < M1; i++) {
@@ -1312,7 +1346,9 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO p
 #pragma unroll
             for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
         }
+        if (ep_part) P.cm.ep_ret[e] = ep.r;
     }
+    if (ep_part) epp.flush(ep_part, ep, __ballot(ep_done) != 0, lane);
 }
 
 // im_roll3_kernel with the observation work moved to a third wave (for small
@@ -1549,6 +1585,15 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
     for (int i = 0; i < M1; i++) nact[i] = (POL || STAGED) ? 0 : io.act[el * M1 + i];
     int64_t dlast = 0;
     bool last_real = false;
+    // episode sink (kernels.hpp EpSink), accumulated in registers over the launch
+    double *const ep_part = P.cm.ep_ret ? P.cm.ep_part + 4 * (e0 / WAVE) : nullptr;
+    EpPart epp;
+    EpLane ep;
+    bool ep_done = false;
+    if (ep_part) {
+        epp.load(ep_part);
+        ep.r = valid ? P.cm.ep_ret[e] : 0.0;
+    }
     wg_lds_sync();   // barrier 0: demand chunk 0 (and its actions when staged, alpha**t) ready
     for (int c = 0; c < nch; c++) {
         const int64_t *db = dbuf + (c % G::RD) * CH * WAVE;
@@ -1581,6 +1626,7 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
                     out_store(io.term + oi, (uint8_t)0);
                     out_store(io.trunc + oi, (uint8_t)0);
                 }
+                if (ep_part) ep.add(0.0, false);   // the reset step's row: reward 0, no flag
                 t = 0;
             } else {
                 const int64_t d = db[kk * WAVE + lane];
@@ -1684,6 +1730,11 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
                         out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.periods ? 1 : 0));   // :350
                     }
                 }
+                if (ep_part) {
+                    const bool done = valid && t + 1 >= P.periods;
+                    ep.add(valid ? reward : 0.0, done);
+                    ep_done |= done;
+                }
                 // age the windows by one period
 #pragma unroll
                 for (int i = 0; i < M1; i++) {
@@ -1717,7 +1768,9 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
 #pragma unroll
             for (int q = 0; q < MD; q++) pol.metrics[e * MD + q] = met[q];
         }
+        if (ep_part) P.cm.ep_ret[e] = ep.r;
     }
+    if (ep_part) epp.flush(ep_part, ep, __ballot(ep_done) != 0, lane);
     TWAIT();
     TPROBE_W(6);
 }
@@ -1739,6 +1792,13 @@ inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / b
 inline bool im_split_applies(const ImParams &p, int t_u, const PolicyIO *pol, const StepIO<int64_t, int64_t> &io) {
     return !pol && io.K == 1 && t_u >= 0 && t_u < p.periods && io.obs &&
            !(p.cm.autoreset == AR_SAME_STEP && t_u + 1 >= p.periods) && p.cm.kn.im_split;
+}
+
+// The lock-step NEXT_STEP reset step (one step at t_u >= periods): its output row
+// is reward 0 with no flag, whose fold changes nothing (EpLane adds +0.0 to
+// returns restarted at +0.0), so the episode sink needs no work for it
+inline bool im_sink_noop(const ImParams &p, int t_u, const PolicyIO *pol, const StepIO<int64_t, int64_t> &io) {
+    return !pol && io.K == 1 && t_u >= p.periods && p.cm.autoreset == AR_NEXT_STEP;
 }
 
 // the 2-/3-role rollout kernels of the reference's default lead times apply
@@ -1807,7 +1867,8 @@ hipError_t im_roll_launch(const ImParams &p, bool backlog, int t_u, const Policy
 // invmgmt_ph.hip: this file compiled a second time for the fast-stream run
 // kernels (a TU of their own, so the two instantiation sets compile in parallel)
 hipError_t im_run_launch_ph(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
-                            const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s) {
+                            const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, bool &sunk, hipStream_t s) {
+    sunk = im_sink_noop(p, t_u, pol, io);
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = (size_t)EPW * M1 * (p.lt_max + 1) * sizeof(int64_t) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
@@ -1835,13 +1896,17 @@ hipError_t im_run_launch_ph(const ImParams &p, int M1, bool backlog, int t_u, co
     } while (0)
         IM_DISPATCH(M1, backlog, S_)
 #undef S_
+        sunk = true;                  // the split kernel folds into the episode sink (if one is set)
         ahead = q.ahead != nullptr;   // every env drew launch step ph_step + 1 into slot cur ^ 1
         if (ahead) slot ^= 1;
         return hipGetLastError();
     }
     // any other launch moves the counter past the cached step: the cache is stale
     ahead = false;
-    if (im_roll_applies(p, M1, t_u, pol, io)) return im_roll_launch<PhiloxGen>(p, backlog, t_u, pol, io, s);
+    if (im_roll_applies(p, M1, t_u, pol, io)) {
+        sunk = true;                  // so do the rollout kernels
+        return im_roll_launch<PhiloxGen>(p, backlog, t_u, pol, io, s);
+    }
 #define K_(M, B, TU, ONE, POL)                                                                          \
     do {                                                                                                \
         if (npd)                                                                                        \
@@ -1871,7 +1936,8 @@ hipError_t im_run_launch_ph(const ImParams &p, int M1, bool backlog, int t_u, co
 INVSIM_PTRS_STATS_TU(im_ph)
 #else
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
-                         const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s) {
+                         const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, bool &sunk, hipStream_t s) {
+    sunk = im_sink_noop(p, t_u, pol, io);
     if (p.cm.N == 0 || io.K <= 0) return hipSuccess;
     const size_t lds = (size_t)EPW * M1 * (p.lt_max + 1) * sizeof(int64_t) + RHS_LDS_MAX * sizeof(double);
     const dim3 grid(grid_for(p.cm.N, EPW)), block(WAVE);
@@ -1879,7 +1945,7 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     const PolicyIO &pv = pol ? *pol : none;
     const bool npd = p.dist >= 2 && p.dist <= 4;
     const bool ph = p.cm.philox != 0;       // fast stream: invmgmt_ph.hip (split / rollout / run kernels, no lookahead)
-    if (ph) return im_run_launch_ph(p, M1, backlog, t_u, pol, io, ahead, slot, s);   // (a cache is the fast stream's)
+    if (ph) return im_run_launch_ph(p, M1, backlog, t_u, pol, io, ahead, slot, sunk, s);   // (a cache is the fast stream's)
     if (im_split_applies(p, t_u, pol, io)) {
         const size_t lds2 = lds + WAVE * sizeof(int64_t);
         const dim3 block2(2 * WAVE);
@@ -1907,6 +1973,7 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     } while (0)
         IM_DISPATCH(M1, backlog, S_)
 #undef S_
+        sunk = true;                  // the split kernel folds into the episode sink (if one is set)
         if (q.ahead) {                // every env drew its next demand into slot cur ^ 1
             ahead = true;
             slot ^= 1;
@@ -1926,7 +1993,10 @@ hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const
     // lock-step rollout of the reference's default lead times: register windows
     // and a demand wave (im_roll3_kernel / im_roll3o_kernel), open loop or with
     // the in-kernel BaseStock / ConstantOrder agents
-    if (im_roll_applies(p, M1, t_u, pol, io)) return im_roll_launch<Pcg>(p, backlog, t_u, pol, io, s);
+    if (im_roll_applies(p, M1, t_u, pol, io)) {
+        sunk = true;                  // so do the rollout kernels
+        return im_roll_launch<Pcg>(p, backlog, t_u, pol, io, s);
+    }
 #define K_(M, B, TU, ONE, POL)                                                                         \
     do {                                                                                                \
         if (npd)                                                                                        \

@@ -130,6 +130,72 @@ struct Common {
     int32_t philox;        // demand stream: 0 numpy PCG64 (parity), 1 fast Philox (PhiloxGen)
     uint64_t ph_step;      // fast stream: the handle's launch-step counter at this launch's first step
     Knobs kn;              // host-side launch choices (read at handle creation)
+    // episode sink (invsim_set_episode_sink), or null: the running return of
+    // every env [N] and the per-64-env-group partials [ceil(N / 64)][4] (EpSink)
+    double *ep_ret;
+    double *ep_part;
+};
+
+// ---------------------------------------------------------------- episode sink
+// The evaluation harness's episodic returns (benchmark_InvManagementBacklogEnv.py:
+// 371, 386, 434: `episode_reward += reward` per step, appended at done) kept on
+// the device.  Per env, in step order over the rows of ONE launch:
+//   ret += reward; all += reward; at terminated | truncated: s += ret,
+//   s2 += ret * ret, c += 1, ret = 0
+// (s, s2, c, all: per-lane accumulators that start at 0 each launch).  At the
+// launch's end each 64-env group g (envs 64 g .. 64 g + 63, one wave) reduces
+// its lanes' four accumulators with one xor butterfly and lane 0 adds them to
+// part[g] = [sum of returns, sum of squares, episodes, sum of rewards] -- a
+// read-modify-write by the group's only owner, so no atomics and a
+// deterministic result.  The fused kernels and the fold kernel
+// (episode_fold_groups_kernel) run this same code, so a launch's fused sink
+// equals the fold of its output rows bit for bit.
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);   // every lane ends with the same sum
+    return v;
+}
+
+struct EpLane {
+    double r = 0.0, s = 0.0, s2 = 0.0, c = 0.0, all = 0.0;
+    __device__ __forceinline__ void add(double rew, bool done) {
+        r += rew;
+        all += rew;
+        if (done) {
+            s += r;
+            s2 += r * r;
+            c += 1.0;
+            r = 0.0;
+        }
+    }
+};
+
+// The group's partials, loaded early (before the launch's other work ends) so
+// the read-modify-write at the end waits for nothing
+struct EpPart {
+    double v[4];
+    __device__ __forceinline__ void load(const double *part_g) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = part_g[j];
+    }
+    // any_done: some lane of the wave folded an episode in this launch (wave-uniform);
+    // without one s, s2, c are 0 in every lane and adding them changes nothing
+    __device__ __forceinline__ void flush(double *part_g, const EpLane &a, bool any_done, int lane) {
+        const double all = wave_sum_f64(a.all);
+        double x[3] = {0.0, 0.0, 0.0};
+        if (any_done) {
+            x[0] = wave_sum_f64(a.s);
+            x[1] = wave_sum_f64(a.s2);
+            x[2] = wave_sum_f64(a.c);
+        }
+        if (lane == 0) {
+            if (any_done) {
+#pragma unroll
+                for (int j = 0; j < 3; j++) part_g[j] = v[j] + x[j];
+            }
+            part_g[3] = v[3] + all;
+        }
+    }
 };
 
 // ---------------------------------------------------------------- Newsvendor
@@ -469,6 +535,9 @@ hipError_t seed_words_launch(const Common &cm, const uint32_t *words, const int3
 hipError_t period_fill_launch(const Common &cm, int32_t t, hipStream_t s);
 hipError_t episode_fold_launch(const double *rew, const uint8_t *term, const uint8_t *trunc, int32_t K,
                                int64_t N, double *ret, double *acc, hipStream_t s);
+// the EpSink fold of K output rows into per-group partials (no atomics)
+hipError_t episode_fold_groups_launch(const double *rew, const uint8_t *term, const uint8_t *trunc, int32_t K,
+                                      int64_t N, double *ret, double *part, hipStream_t s);
 
 hipError_t nv_reset_launch(const NvParams &p, const uint8_t *mask, float *obs, hipStream_t s);
 // ahead / slot: the demand lookahead cache state, as for im_run_launch
@@ -483,12 +552,14 @@ hipError_t im_reset_launch(const ImParams &p, int M1, bool backlog, const uint8_
                            int64_t *obs, hipStream_t s);
 // ahead: in = lookahead slot `slot` holds every env's next demand; out = the
 // slot (updated) does now
+// sunk: out = the launched kernel folded its rows into the episode sink
+// (Common::ep_ret), or had nothing to fold; else the caller folds the outputs
 hipError_t im_run_launch(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
-                         const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s);
+                         const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, bool &sunk, hipStream_t s);
 // the fast-stream (cm.philox) kernels, invmgmt_ph.hip; ahead / slot: the
 // fast stream's demand-only lookahead cache (never committed: it holds no state)
 hipError_t im_run_launch_ph(const ImParams &p, int M1, bool backlog, int t_u, const PolicyIO *pol,
-                            const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, hipStream_t s);
+                            const StepIO<int64_t, int64_t> &io, bool &ahead, int &slot, bool &sunk, hipStream_t s);
 // cm.rng <- the committed generator state held by the lookahead cache (whose
 // current slot is `slot`); needed before anything reads cm.rng while it is valid
 hipError_t im_commit_launch(const ImParams &p, int slot, hipStream_t s);

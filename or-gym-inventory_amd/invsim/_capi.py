@@ -28,8 +28,9 @@ EXPORTS = (
     "invsim_state_field", "invsim_get_state", "invsim_set_state", "invsim_episode_fold",
     "invsim_debug_ptrs_stats", "invsim_set_demand_stream", "invsim_demand_stream",
     "invsim_capture_begin", "invsim_capture_end", "invsim_position",
+    "invsim_episode_fold_groups", "invsim_set_episode_sink",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 DEMAND_STREAMS = {"numpy": 0, "philox": 1}
 
 
@@ -105,6 +106,8 @@ def _declare(lib):
         "invsim_get_state": ([H, P, P], C.c_int),
         "invsim_set_state": ([H, P, P], C.c_int),
         "invsim_episode_fold": ([P, P, P, I32, I64, P, P, P], C.c_int),
+        "invsim_episode_fold_groups": ([P, P, P, I32, I64, P, P, P], C.c_int),
+        "invsim_set_episode_sink": ([H, P, P], C.c_int),
         "invsim_debug_ptrs_stats": ([P, I32], C.c_int),
         "invsim_set_demand_stream": ([H, I32], C.c_int),
         "invsim_demand_stream": ([H, P], C.c_int),

@@ -7,7 +7,7 @@ every env's trajectory identical for any W.  The only collective is the
 episodic-return reduction the harness reports (mean / std / count of episode
 returns, ``benchmark_InvManagementBacklogEnv.py:389-440``): ONE all-reduce of
 four f64 over RCCL (torch.distributed "nccl" backend on ROCm), latency-bound
-at 32 bytes.
+at 32 bytes, after each rank sums its per-group partials.
 """
 import torch
 import torch.distributed as dist
@@ -25,13 +25,18 @@ def shard_range(global_envs, rank, world):
 
 class EpisodeStats:
     """Accumulates per-env returns; folds finished episodes into
-    acc = [sum, sum of squares, episodes, sum of all rewards] and all-reduces
-    acc across ranks.
+    [sum, sum of squares, episodes, sum of all rewards] and all-reduces them
+    across ranks.
 
-    Device tensors are folded by the HIP kernel ``invsim_episode_fold`` (one
-    launch per block of K steps, reading the step outputs where the env wrote
-    them).  Host tensors (a CPU rehearsal stepping the oracle) are folded with
-    the same arithmetic in torch: there is no device data to hand the kernel.
+    Device statistics are kept as per-64-env-group partials ``part``
+    [ceil(N / 64), 4] (``acc`` is their column sum): either folded from output
+    rows by the HIP kernel ``invsim_episode_fold_groups`` (``update_block``),
+    or folded inside the step / rollout kernels themselves once the stats are
+    attached to an env as its episode sink (``attach``, ``invsim_set_episode_sink``),
+    which is the same arithmetic with no second pass over the outputs.  Host
+    tensors (a CPU rehearsal stepping the oracle) are folded with the same
+    arithmetic in torch into a single row: there is no device data to hand the
+    kernel.
     """
 
     def __init__(self, num_envs, device):
@@ -41,11 +46,37 @@ class EpisodeStats:
         self.device = dev
         self.num_envs = int(num_envs)
         self.ret = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
-        self.acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+        groups = (self.num_envs + 63) // 64 if dev.type == "cuda" else 1
+        self.part = torch.zeros((max(groups, 1), 4), dtype=torch.float64, device=self.device)
+        self._env = None
+
+    @property
+    def acc(self):
+        """[sum of finished-episode returns, sum of their squares, episodes, sum of rewards]"""
+        return self.part.sum(0)
 
     def reset_acc(self):
         """Forget the folded episodes; running returns carry on."""
-        self.acc.zero_()
+        self.part.zero_()
+
+    def attach(self, env):
+        """Make these statistics `env`'s episode sink: every step / rollout of
+        the env folds its rows here on the device (invsim_set_episode_sink)."""
+        from . import _capi
+        if self.device.type != "cuda" or env.device != self.device or env.num_envs != self.num_envs:
+            raise ValueError("EpisodeStats.attach: a CUDA EpisodeStats of the env's device and size")
+        _capi.check(_capi.lib().invsim_set_episode_sink(env._h, self.ret.data_ptr(), self.part.data_ptr()),
+                    env._h, "invsim_set_episode_sink")
+        self._env = env
+        env._episode_sink = self           # the env's kernels write ret / part: keep them alive with it
+
+    def detach(self):
+        if self._env is not None:
+            from . import _capi
+            _capi.check(_capi.lib().invsim_set_episode_sink(self._env._h, None, None), self._env._h,
+                        "invsim_set_episode_sink")
+            self._env._episode_sink = None
+            self._env = None
 
     def update(self, reward, done):
         """reward [N] f64, done [N] bool (terminated | truncated) of one step."""
@@ -69,9 +100,9 @@ class EpisodeStats:
             with torch.cuda.device(self.device):           # the launch goes to the stats' GPU
                 if stream is None:
                     stream = torch._C._cuda_getCurrentRawStream(self.device.index)
-                _capi.check(_capi.lib().invsim_episode_fold(
+                _capi.check(_capi.lib().invsim_episode_fold_groups(
                     reward.data_ptr(), ptr(terminated), ptr(truncated), K, N, self.ret.data_ptr(),
-                    self.acc.data_ptr(), stream), None, "invsim_episode_fold")
+                    self.part.data_ptr(), stream), None, "invsim_episode_fold_groups")
             return
         done = torch.zeros((K, N), dtype=torch.bool)
         for f in flags:
@@ -80,7 +111,7 @@ class EpisodeStats:
             self.ret += reward[k]
             d = done[k].to(torch.float64)
             r = self.ret * d
-            self.acc += torch.stack([r.sum(), (r * r).sum(), d.sum(), reward[k].sum()])
+            self.part[0] += torch.stack([r.sum(), (r * r).sum(), d.sum(), reward[k].sum()])
             self.ret *= (1.0 - d)
 
     def allreduce(self, group=None):

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     missing = [f for f in declared if not hasattr(lib, f)]
     assert not missing, missing
     assert sorted(_capi.EXPORTS) == declared
-    assert lib.invsim_abi_version() == 3
+    assert lib.invsim_abi_version() == 4
 
 
 def test_library_is_gfx950_code_object():
