@@ -90,10 +90,13 @@ def parse():
                          "kernels fold in-kernel), inline = a fold launch between blocks on the kernel "
                          "stream (auto for the other families), side = that fold on a side stream "
                          "(measured slower), none = off (A/B only: no episode_stats)")
-    ap.add_argument("--stop", default="event", choices=["event", "sync"],
-                    help="end of the timed region: the kernel stream's last event completing (default), or "
-                         "torch.cuda.synchronize returning; the region is closed by torch.cuda.synchronize "
-                         "either way")
+    ap.add_argument("--stop", default="spin", choices=["event", "spin", "sync"],
+                    help="end of the timed region: the kernel stream's last event completing, waited for "
+                         "by polling hipEventQuery (spin, default: measured 1-2 %% higher on the 20-step "
+                         "driver line than hipEventSynchronize, profiles/r06/stop_ab) or with "
+                         "hipEventSynchronize (event), or "
+                         "torch.cuda.synchronize returning (sync); the region is closed by "
+                         "torch.cuda.synchronize either way")
     ap.add_argument("--no-graph-line", action="store_true",
                     help="step mode: skip the HIP-graph replay region reported under 'graph'")
     ap.add_argument("--no-rollout-line", action="store_true",
@@ -210,14 +213,20 @@ def _fold_rows(stats, rew, term, trunc, rows, sp):
         stats.update_block(rew[:rows], term[:rows], trunc[:rows], stream=sp)
 
 
-def fold_mode(args, env):
-    """--fold auto: the in-kernel episode sink where the family's step and
-    rollout kernels fold in-kernel (InvMgmt), else the fold launch between
-    blocks (the library would otherwise fold each launch's rows separately)."""
+def fold_mode(args, env, mode="step"):
+    """--fold auto: K-step rollouts of InvMgmt fold inside the rollout kernels
+    (the episode sink: the running return is read and written once per launch,
+    16 B per env per K steps, and no second pass reads the outputs); single
+    steps fold their output rows in one launch per block of steps (10 B per
+    env-step of reward and flags, against the sink's 16 B of running return
+    per env-step: measured 8.12 vs 8.51 us per step at 65 536 envs,
+    profiles/r06/sink); the other families always fold per block (their kernels
+    have no in-kernel fold, and the library would fold each launch's rows
+    separately)."""
     import invsim
     if args.fold != "auto":
         return args.fold
-    return "sink" if env.family == invsim._capi.INVSIM_INVMGMT else "inline"
+    return "sink" if env.family == invsim._capi.INVSIM_INVMGMT and mode != "step" else "inline"
 
 
 def _span(t0, t1, dev, dist):
@@ -274,7 +283,7 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     po = obs.data_ptr()
     slab_ptrs = [(rew[b].data_ptr(), term[b].data_ptr(), trunc[b].data_ptr()) for b in range(2)]
     stats = EpisodeStats(N, dev)
-    fm = fold_mode(args, env)
+    fm = fold_mode(args, env, mode)
     if fm == "sink":           # the step / rollout kernels fold their rows into `stats` themselves
         stats.attach(env)
     fstream = torch.cuda.Stream(dev)
@@ -369,14 +378,18 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     region(calls, True)
-    if args.stop == "event":
+    if args.stop in ("event", "spin"):
         # the end of the work is `stream`'s last event completing
         # (hipEventSynchronize, no device-wide drain); with --fold side the last
         # block's fold runs on fstream, so `stream` waits for it first
         if fm == "side":
             stream.wait_stream(fstream)
         end_ev.record(stream)
-        end_ev.synchronize()
+        if args.stop == "spin":
+            while not end_ev.query():
+                pass
+        else:
+            end_ev.synchronize()
         t1 = time.perf_counter()
         torch.cuda.synchronize(dev)
     else:

@@ -259,7 +259,7 @@ int invsim_episode_fold(const double *reward, const uint8_t *terminated, const u
  * sum of their squares, finished episodes, sum of every reward folded] of envs
  * 64 g .. 64 g + 63.  Per env, in row order: ret += reward; at terminated |
  * truncated the return is folded and restarts at 0; each group's per-lane sums
- * over the K rows are then reduced by one xor butterfly and added to part[g].
+ * over the K rows are then reduced in a fixed order and added to part[g].
  * The statistics are the column sums of part. */
 int invsim_episode_fold_groups(const double *reward, const uint8_t *terminated, const uint8_t *truncated,
                                int32_t K, int64_t n_envs, double *ret, double *part, void *stream);

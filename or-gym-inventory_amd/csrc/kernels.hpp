@@ -144,16 +144,40 @@ struct Common {
 //   s2 += ret * ret, c += 1, ret = 0
 // (s, s2, c, all: per-lane accumulators that start at 0 each launch).  At the
 // launch's end each 64-env group g (envs 64 g .. 64 g + 63, one wave) reduces
-// its lanes' four accumulators with one xor butterfly and lane 0 adds them to
+// its lanes' four accumulators (wave_sum_f64) and lane 0 adds them to
 // part[g] = [sum of returns, sum of squares, episodes, sum of rewards] -- a
 // read-modify-write by the group's only owner, so no atomics and a
 // deterministic result.  The fused kernels and the fold kernel
 // (episode_fold_groups_kernel) run this same code, so a launch's fused sink
 // equals the fold of its output rows bit for bit.
+// The wave's sum of v, the same value in every lane (all 64 lanes active):
+// within each 16-lane row a DPP butterfly (quad_perm xor 1, xor 2, then
+// row_half_mirror and row_mirror: each pairs lanes holding partial sums of
+// disjoint lane sets, and x + y == y + x exactly, so every lane of the row ends
+// with the same row sum), then the four row sums read from lanes 0, 16, 32 and
+// 48 and added as (r0 + r1) + (r2 + r3).  Tens of cycles of dependent VALU
+// work; the first version, a six-level ds_bpermute butterfly (__shfl_xor of
+// each half), made the sink cost the InvMgmt step 0.55 us (measured, 65 536
+// envs), most of it that chain's LDS round trips at the dynamics wave's tail.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);   // every lane ends with the same sum
-    return v;
+    v += dpp_f64<0xB1>(v);     // quad_perm [1, 0, 3, 2]: lane ^ 1
+    v += dpp_f64<0x4E>(v);     // quad_perm [2, 3, 0, 1]: lane ^ 2
+    v += dpp_f64<0x141>(v);    // row_half_mirror: lane i <-> 7 - i within 8
+    v += dpp_f64<0x140>(v);    // row_mirror: lane i <-> 15 - i within 16
+    return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
 struct EpLane {
