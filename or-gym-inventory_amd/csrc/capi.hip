@@ -216,11 +216,15 @@ Knobs read_knobs() {
     k.im_ahead = env_flag("INVSIM_IM_AHEAD", k.im_ahead);
     if (const char *v = std::getenv("INVSIM_IM_ROLL3O_G2"); v && (v[0] == '0' || v[0] == '1'))
         k.im_roll3o_g2 = (int8_t)(v[0] - '0');
-    if (const char *v = std::getenv("INVSIM_IM_ROLL3O_MAX_N"); v && v[0]) {   // a decimal count, else the default
-        char *end = nullptr;
-        const long long x = std::strtoll(v, &end, 10);
-        if (end && !*end && x >= 0) k.im_roll3o_max_n = (int64_t)x;
-    }
+    auto count = [](const char *name, int64_t &dst) {   // a decimal count, else the default
+        if (const char *v = std::getenv(name); v && v[0]) {
+            char *end = nullptr;
+            const long long x = std::strtoll(v, &end, 10);
+            if (end && !*end && x >= 0) dst = (int64_t)x;
+        }
+    };
+    count("INVSIM_IM_ROLL3O_MAX_N", k.im_roll3o_max_n);
+    count("INVSIM_NET_ROLLQ_MAX_N", k.net_rollq_max_n);
     k.nv_xcd = env_flag("INVSIM_NV_XCD", k.nv_xcd);
     k.nv_roll = env_flag("INVSIM_NV_ROLL", k.nv_roll);
     k.nv_pol_roll = env_flag("INVSIM_NV_POL_ROLL", k.nv_pol_roll);

@@ -1364,6 +1364,453 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO po
     }
 }
 
+// ---------------------------------------------------------------- small shards
+// The K-step rollout for small per-GPU shards (config 5 split over 8 GPUs:
+// 4 096 envs per rank).  There the 3-role kernel runs one dynamics wave per
+// 64 envs on 64 of the 1 024 SIMDs, and each of those waves issues the whole
+// step, ~425 instructions of which 240 are f64 (half rate on MI355X: 8 cycles
+// per wave instruction), one env per lane: 1.3 us per step, with the demand
+// draws and the observation work hidden beside it (ablation builds,
+// profiles/r06/net_small/ablation.txt).  Fewer envs per wave do not shorten
+// that chain; spreading ONE env's edge work over lanes does.
+//
+// net_rollq_kernel: one 16-lane DPP row per env, 4 envs per dynamics wave.
+// Lane l of an env's row is reorder link l (l < E) and main node l (l < J):
+//   * order fulfilment (:448-490): every link lane evaluates its own order in
+//     the same instructions.  Links of one supplier are consecutive and
+//     draw on the supplier's running consumption in link order, so the
+//     lanes run in rounds by their rank within the supplier: round r's lanes
+//     take the consumption of lane l - 1 (DPP row_shr:1) from round r - 1 --
+//     a segmented clamp-scan in the reference's order;
+//   * pipeline and arrivals (:494-528): each link lane keeps its own order
+//     ring in LDS and updates its pipeline Y; node lane j gathers its
+//     predecessor links' arrivals (ds_bpermute within the row) and adds them
+//     in predecessor-adjacency order, then subtracts the supplier
+//     consumption of its last link;
+//   * market fulfilment (:536-566) on the lane of the market's node;
+//   * profit (:578-613): link lanes form lp * R and lg * max(0, Y); node lane
+//     j gathers its successors' and predecessors' terms in the same sum
+//     orders as spec_core and forms its node profit; the period total is a
+//     sequential scan over the node lanes in node order (row_shr:1, J - 1
+//     steps), the reference's `total_profit_period += node_profit`.
+// Every sum keeps spec_core's operand order, so results are bit-identical.
+// Roles per 16-env workgroup: wave 0 draws the demands (net_demand_loop, one
+// env per lane), wave 1 builds the observations one chunk behind (as
+// net_roll3o_kernel's obs wave), waves 2-5 are the dynamics waves.
+template <class G>
+struct NetQ {
+    static constexpr int QE = 16;                              // envs per workgroup
+    static constexpr int QW = 4;                               // dynamics waves (4 envs each)
+    static_assert(G::E <= 16 && G::J <= 16, "one 16-lane row per env");
+    static constexpr int sup_rank(int k) {                     // rank of link k among its supplier's links
+        int r = 0;
+        for (int q = 0; q < k; q++) r += (G::sup[k] >= 0 && G::sup[q] == G::sup[k]) ? 1 : 0;
+        return r;
+    }
+    static constexpr bool sup_consecutive() {                  // a supplier's links are adjacent
+        for (int k = 1; k < G::E; k++)
+            if (G::sup[k] >= 0 && sup_rank(k) > 0 && G::sup[k - 1] != G::sup[k]) return false;
+        return true;
+    }
+    static_assert(sup_consecutive(), "the clamp-scan takes a supplier's links as consecutive lanes");
+    static constexpr int rmax() {
+        int m = 0;
+        for (int k = 0; k < G::E; k++) m = sup_rank(k) + 1 > m ? sup_rank(k) + 1 : m;
+        return m;
+    }
+    static constexpr int last_link(int j) {                    // the supplier's last link, or -1
+        int l = -1;
+        for (int k = 0; k < G::E; k++) l = G::sup[k] == j ? k : l;
+        return l;
+    }
+    static constexpr int market(int j) {                       // the market of node j, or -1
+        int m = -1;
+        for (int r = 0; r < G::RL; r++) m = G::rl_node[r] == j ? r : m;
+        return m;
+    }
+    static constexpr bool one_market_per_node() {
+        for (int j = 0; j < G::J; j++) {
+            int n = 0;
+            for (int r = 0; r < G::RL; r++) n += G::rl_node[r] == j ? 1 : 0;
+            if (n > 1) return false;
+        }
+        return true;
+    }
+    static_assert(one_market_per_node(), "a node lane serves at most one market");
+    static constexpr int pmax() {
+        int m = 0;
+        for (int j = 0; j < G::J; j++) m = G::pred_ptr[j + 1] - G::pred_ptr[j] > m ? G::pred_ptr[j + 1] - G::pred_ptr[j] : m;
+        return m;
+    }
+    static constexpr int smax() {
+        int m = 0;
+        for (int j = 0; j < G::J; j++) m = G::succ_ptr[j + 1] - G::succ_ptr[j] > m ? G::succ_ptr[j + 1] - G::succ_ptr[j] : m;
+        return m;
+    }
+    static constexpr int NR = G::RL + G::J + NetLpos<G>::count();   // obs record columns per step
+    // chunk of 4 launch steps: the dynamics lanes load chunk c + 1's actions at
+    // the start of chunk c, 4-7 steps before their use (a load one step ahead
+    // waits, in vmcnt order, behind the previous step's stores)
+    static constexpr int CH = 4, RD = 4;
+    static constexpr int AP = 256;                             // alpha**t in LDS (T <= AP)
+    static constexpr size_t tile_bytes() { return (size_t)((QE * G::O + 3) / 4) * 4 * sizeof(float); }
+    static constexpr size_t rhs_bytes() { return (size_t)G::RL * RHS_LDS_MAX * sizeof(double); }
+    static constexpr size_t dbuf_bytes() { return (size_t)RD * CH * G::RL * WAVE * sizeof(double); }
+    static constexpr size_t ring_bytes() { return (size_t)(G::sumL > 0 ? G::sumL : 1) * QE * sizeof(double); }
+    static constexpr size_t rec_bytes() { return 2 * (size_t)CH * NR * WAVE * sizeof(float); }
+    static constexpr size_t lds() {
+        return tile_bytes() + rhs_bytes() + dbuf_bytes() + ring_bytes() + rec_bytes() + AP * sizeof(double);
+    }
+};
+
+// a per-lane constant: f(i) of this lane's index i (< n), else dflt (a select chain, once per launch)
+template <int n, class T, class F>
+__device__ __forceinline__ T lane_const(int i, T dflt, F f) {
+    T v = dflt;
+#pragma unroll
+    for (int q = 0; q < n; q++)
+        if (i == q) v = f(q);
+    return v;
+}
+
+// lane (row base + src)'s value (ds_bpermute within the env's row)
+__device__ __forceinline__ double row_get(double v, int rowbase, int src) { return __shfl(v, rowbase + src); }
+
+// lane l - 1's value within a 16-lane row (DPP row_shr:1; lane 0 of a row gets 0)
+__device__ __forceinline__ double row_shr1(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x111, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x111, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+template <class G, class RG = Pcg>
+__global__ void __launch_bounds__(6 * WAVE)
+net_rollq_kernel(NetParams P, int t_start, StepIO<float, float> io) {
+    using Q = NetQ<G>;
+    using LP = NetLpos<G>;
+    constexpr int O = G::O, CH = Q::CH, RD = Q::RD, RL = G::RL, NR = Q::NR, QE = Q::QE, E = G::E, J = G::J;
+    constexpr int TILE_IT = (QE * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
+    extern __shared__ __attribute__((aligned(16))) float nq_lds[];
+    char *lb = reinterpret_cast<char *>(nq_lds);
+    float *tile = nq_lds;
+    double *rhs_l = reinterpret_cast<double *>(lb + Q::tile_bytes());
+    double *dbuf = reinterpret_cast<double *>(lb + Q::tile_bytes() + Q::rhs_bytes());       // [RD * CH][RL][WAVE]
+    double *ring = reinterpret_cast<double *>(lb + Q::tile_bytes() + Q::rhs_bytes() + Q::dbuf_bytes());   // [sumL][QE]
+    float *rec = reinterpret_cast<float *>(lb + Q::tile_bytes() + Q::rhs_bytes() + Q::dbuf_bytes() +
+                                           Q::ring_bytes());                                // [2][CH][NR][WAVE]
+    double *ap_l = reinterpret_cast<double *>(lb + Q::tile_bytes() + Q::rhs_bytes() + Q::dbuf_bytes() +
+                                              Q::ring_bytes() + Q::rec_bytes());            // alpha**t, t < T
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int w = threadIdx.x / WAVE;
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    const int64_t e0 = (int64_t)blockIdx.x * QE;
+    const int nvalid = (int)((N - e0) < QE ? (N - e0) : QE);
+    const int K = io.K;
+    const int nch = (K + CH - 1) / CH;
+    if (w < 2) {
+        // one env per lane (lanes >= QE repeat lane & (QE - 1)'s env and store nothing)
+        const int q = lane & (QE - 1);
+        const int64_t e = e0 + q;
+        const bool valid = lane < QE && e < N;
+        const int64_t el = e < N ? e : N - 1;
+        if (w == 0) {   // ---- demand wave (as net_roll3o_kernel's)
+            PtrsConst pc[RL];
+#pragma unroll
+            for (int r = 0; r < RL; r++) pc[r] = P.rl_pc[r];
+            constexpr int NT = RHS_LDS_MAX / WAVE;
+            double tv[RL][NT];
+#pragma unroll
+            for (int r = 0; r < RL; r++) {
+                const int qm = pc[r].nk > 0 ? pc[r].nk - 1 : 0;
+                const double *src = pc[r].nk > 0 ? P.rhs + pc[r].toff : P.alpha_pow;   // any valid pointer
+#pragma unroll
+                for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
+            }
+            RG g;
+            P.cm.rng.load(el, g);
+#pragma unroll
+            for (int r = 0; r < RL; r++)
+#pragma unroll
+                for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
+            wave_lds_sync();
+            net_demand_loop<G, CH, RD>(g, pc, rhs_l, dbuf, lane, K, nch + 1, t_start, P.T, P.cm.ph_step);
+            if (valid) P.cm.rng.store_state(e, g);
+            return;
+        }
+        // ---- obs wave (as net_roll3o_kernel's, QE envs)
+        float *trow = tile + q * O;
+        int t = t_start;
+        float wf[LP::sumL1() > 0 ? LP::sumL1() : 1];
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+            if (G::L[k] <= 1) continue;
+#pragma unroll
+            for (int a = 1; a < G::L[k]; a++) {
+                const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+                const double v = P.Rring[(int64_t)row * S + el];
+                wf[LP::woff(k) + a - 1] = (t - a >= 0) ? (float)v : 0.f;
+            }
+        }
+        net_wg_sync();   // barrier 0
+        for (int c = 0; c < nch; c++) {
+            net_wg_sync();   // barrier c + 1: record chunk c ready
+            const float *rb = rec + (c & 1) * CH * NR * WAVE;
+            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+                const int k = c * CH + kk;
+#ifdef INVSIM_ABL_R3_NO_OBS
+                continue;
+#endif
+                if (lane < QE) {
+                    if (t >= P.T) {                    // NEXT_STEP autoreset: [0, I0, 0 ...] (:301-332)
+#pragma unroll
+                        for (int r = 0; r < RL; r++) trow[r] = 0.f;
+#pragma unroll
+                        for (int j = 0; j < J; j++) trow[RL + j] = (float)G::I0[j];
+#pragma unroll
+                        for (int x = 0; x < G::sumL; x++) trow[RL + J + x] = 0.f;
+#pragma unroll
+                        for (int x = 0; x < LP::sumL1(); x++) wf[x] = 0.f;
+                    } else {
+#pragma unroll
+                        for (int x = 0; x < RL + J; x++) trow[x] = rb[(kk * NR + x) * WAVE + q];
+#pragma unroll
+                        for (int kl = 0; kl < E; kl++) {
+                            if (G::L[kl] == 0) continue;
+                            const float rn = rb[(kk * NR + RL + J + LP::rank(kl)) * WAVE + q];
+#pragma unroll
+                            for (int p = 0; p + 1 < G::L[kl]; p++)
+                                trow[G::win_off[kl] + p] = wf[LP::woff(kl) + (G::L[kl] - 1 - p) - 1];
+                            trow[G::win_off[kl] + G::L[kl] - 1] = rn;
+#pragma unroll
+                            for (int a = G::L[kl] - 1; a >= 2; a--) wf[LP::woff(kl) + a - 1] = wf[LP::woff(kl) + a - 2];
+                            if (G::L[kl] > 1) wf[LP::woff(kl)] = rn;
+                        }
+                    }
+                }
+                t = (t >= P.T) ? 0 : t + 1;
+                wave_lds_sync();
+#ifndef INVSIM_ABL_ROLL_NO_STORE
+                store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+#endif
+                wave_lds_sync();
+            }
+        }
+        return;
+    }
+    // ---- dynamics waves: env row (lane >> 4), lane l = link l / node l of that env
+    const int l = lane & 15;
+    const int rowbase = lane & ~15;
+    const int q = (w - 2) * 4 + (lane >> 4);                 // env within the workgroup
+    const int64_t e = e0 + q;
+    const bool valid = e < N;
+    const int64_t el = valid ? e : N - 1;
+    // link-lane constants (lanes >= E: a raw-material link that orders nothing)
+    const bool is_link = l < E;
+    const int lk = is_link ? l : 0;
+    const int sup = lane_const<E>(l, -1, [](int k) { return G::sup[k]; });
+    const int supc = sup < 0 ? 0 : sup;
+    const bool sfac = lane_const<E>(l, 0, [](int k) { return G::sup_is_factory[k]; }) != 0;
+    const double Csp = lane_const<E>(l, 0.0, [](int k) { return G::C[G::sup[k] < 0 ? 0 : G::sup[k]]; });
+    const double vsp = lane_const<E>(l, 1.0, [](int k) { return G::v[G::sup[k] < 0 ? 0 : G::sup[k]]; });
+    const int Lk = lane_const<E>(l, 0, [](int k) { return G::L[k]; });
+    const int roff = lane_const<E>(l, 0, [](int k) { return G::ring_off[k]; });
+    const double lpk = lane_const<E>(l, 0.0, [](int k) { return G::lp[k]; });
+    const double lgk = lane_const<E>(l, 0.0, [](int k) { return G::lg[k]; });
+    const int rank = lane_const<E>(l, 0, [](int k) { return Q::sup_rank(k); });
+    const int reccol = lane_const<E>(l, -1, [](int k) { return G::L[k] > 0 ? RL + J + LP::rank(k) : -1; });
+    // node-lane constants
+    const bool is_node = l < J;
+    const double I0j = lane_const<J>(l, 0.0, [](int j) { return G::I0[j]; });
+    const double hj = lane_const<J>(l, 0.0, [](int j) { return G::h[j]; });
+    const double oj = lane_const<J>(l, 0.0, [](int j) { return G::o[j]; });
+    const double vj = lane_const<J>(l, 1.0, [](int j) { return G::v[j]; });
+    const bool facj = lane_const<J>(l, 0, [](int j) { return G::is_factory[j]; }) != 0;
+    const bool retj = lane_const<J>(l, 0, [](int j) { return G::is_retail[j]; }) != 0;
+    const int lastl = lane_const<J>(l, -1, [](int j) { return Q::last_link(j); });
+    const int mkt = lane_const<J>(l, -1, [](int j) { return Q::market(j); });
+    const int mk = mkt < 0 ? 0 : mkt;
+    const double rlp = lane_const<RL>(mk, 0.0, [](int r) { return G::rl_p[r]; });
+    const double rlb = lane_const<RL>(mk, 0.0, [](int r) { return G::rl_b[r]; });
+    constexpr int PM = Q::pmax() > 0 ? Q::pmax() : 1, SM = Q::smax() > 0 ? Q::smax() : 1;
+    const int npred = lane_const<J>(l, 0, [](int j) { return G::pred_ptr[j + 1] - G::pred_ptr[j]; });
+    const int nsucc = lane_const<J>(l, 0, [](int j) { return G::succ_ptr[j + 1] - G::succ_ptr[j]; });
+    int pidx[PM], sidx[PM > SM ? PM : SM], skind[SM];
+#pragma unroll
+    for (int x = 0; x < PM; x++)
+        pidx[x] = lane_const<J>(l, 0, [x](int j) {
+            return G::pred_ptr[j] + x < G::pred_ptr[j + 1] ? G::pred_idx[G::pred_ptr[j] + x] : 0;
+        });
+#pragma unroll
+    for (int x = 0; x < SM; x++) {
+        sidx[x] = lane_const<J>(l, 0, [x](int j) {
+            return G::succ_ptr[j] + x < G::succ_ptr[j + 1] ? G::succ_idx[G::succ_ptr[j] + x] : 0;
+        });
+        skind[x] = lane_const<J>(l, 0, [x](int j) {
+            return G::succ_ptr[j] + x < G::succ_ptr[j + 1] ? G::succ_kind[G::succ_ptr[j] + x] : 0;
+        });
+    }
+    // state: X (node lanes), U (the node's market), Y (link lanes), order ring (link lanes, LDS)
+    int t = t_start;
+    double X = is_node ? P.X[(int64_t)l * S + el] : 0.0;
+    double U = (is_node && mkt >= 0) ? P.U[(int64_t)mk * S + el] : 0.0;
+    double Y = is_link ? P.Y[(int64_t)lk * S + el] : 0.0;
+    double *rg = ring + q;                                   // [sumL][QE]
+    for (int a = 0; a < (is_link ? Lk : 0); a++) rg[(roff + a) * QE] = P.Rring[(int64_t)(roff + a) * S + el];
+    int pos = Lk > 0 ? (int)((uint32_t)t % (uint32_t)Lk) : 0;   // ring slot of R[t - L] / R[t]
+    if (w == 2)
+        for (int x = lane; x < P.T; x += WAVE) ap_l[x] = P.alpha_pow[x];   // before barrier 0
+    // this chunk's actions (acur) and the next one's (anxt), link lanes
+    float acur[CH], anxt[CH];
+#pragma unroll
+    for (int i = 0; i < CH; i++) acur[i] = io.act[((int64_t)(i < K ? i : K - 1) * N + el) * E + lk];
+    net_wg_sync();   // barrier 0: demand chunk 0 ready (and every ring row and alpha**t in LDS)
+    for (int c = 0; c < nch; c++) {
+        const double *db = dbuf + (c % RD) * CH * RL * WAVE;
+        float *rb = rec + (c & 1) * CH * NR * WAVE;
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+            const int kn = (c + 1) * CH + i;
+            anxt[i] = io.act[((int64_t)(kn < K ? kn : K - 1) * N + el) * E + lk];
+        }
+#pragma unroll
+        for (int kk = 0; kk < CH; kk++) {
+            const int k = c * CH + kk;
+            if (k >= K) break;
+            const int64_t oi = (int64_t)k * N + e;
+            const float act = acur[kk];
+            const double apow = ap_l[t < P.T ? t : 0];
+            if (t >= P.T) {                                   // NEXT_STEP autoreset (:301-332)
+                X = I0j;
+                U = 0.0;
+                Y = 0.0;
+                if (valid && l == J - 1) {
+                    out_store(io.rew + oi, 0.0);
+                    out_store(io.term + oi, (uint8_t)0);
+                    out_store(io.trunc + oi, (uint8_t)0);
+                }
+                t = 0;
+                pos = 0;
+                continue;
+            }
+#ifdef INVSIM_ABL_Q_NO_DYN   // profiling ablation only (wrong results): the dynamics waves idle
+            t += 1;
+            continue;
+#endif
+            // 0) orders (:448-490): a clamp-scan over each supplier's consecutive link lanes.
+            // Branch-free: every lane evaluates every round and keeps its own round's
+            // result (selects), so the row gathers are not split by exec-mask branches
+            const double Xs = row_get(X, rowbase, supc);      // the supplier's on-hand X[t]
+            const double rq = rint((double)act);
+            const double request = (rq > 0) ? rq : 0.0;
+            double cons = 0.0, Rn = 0.0;
+#pragma unroll
+            for (int r = 0; r < Q::rmax(); r++) {
+                const double cin = (r == 0) ? 0.0 : row_shr1(cons);
+                const double oav = max0(Xs - cin);
+                double avail = oav;
+                const double mpi = vsp * oav;
+                const double mp = (mpi < Csp) ? mpi : Csp;
+                avail = (sfac && mp < avail) ? mp : avail;
+                const double f = (avail < request) ? avail : request;
+                const double cn = cin + f / vsp;
+                const bool mine = rank == r;
+                Rn = mine ? (sup < 0 ? request : f) : Rn;     // raw material: unlimited
+                cons = (mine && sup >= 0) ? cn : cons;
+            }
+            Rn = is_link ? Rn : 0.0;
+            // 1) pipeline (:494-511): arrival R[t - L] (age L) from the lane's ring, or R[t] when L == 0
+            const int slot = (roff + pos) * QE;               // lanes with L == 0 touch their row 0 (unused)
+            const double wa = rg[slot];
+            const double arrv = (Lk == 0) ? Rn : ((t >= Lk) ? wa : 0.0);
+            if (Lk > 0) rg[slot] = Rn;                        // R[t] replaces R[t - L] in the same slot
+            pos = (pos + 1 >= Lk) ? 0 : pos + 1;
+            Y = Y - arrv + Rn;
+            const double lpR = lpk * Rn;                      // purchasing / sales term of the link
+            const double lgY = lgk * max0(Y);                 // pipeline holding term of the link
+            // every row gather of the node phase at once (all depend only on the link phase)
+            double g_arr[PM], g_lpR[PM], g_lgY[PM], g_sR[SM], g_sP[SM];
+#pragma unroll
+            for (int x = 0; x < PM; x++) {
+                g_arr[x] = row_get(arrv, rowbase, pidx[x]);
+                g_lpR[x] = row_get(lpR, rowbase, pidx[x]);
+                g_lgY[x] = row_get(lgY, rowbase, pidx[x]);
+            }
+#pragma unroll
+            for (int x = 0; x < SM; x++) {
+                g_sR[x] = row_get(Rn, rowbase, sidx[x]);
+                g_sP[x] = row_get(lpR, rowbase, sidx[x]);
+            }
+            const double cj = row_get(cons, rowbase, lastl < 0 ? 0 : lastl);
+            // arrivals in predecessor order (:516-523), X[t+1] (:528).  Masked terms add
+            // +0.0, which leaves these sums unchanged: they start at +0.0 and so are never -0.0
+            double acc = 0.0;
+#pragma unroll
+            for (int x = 0; x < PM; x++) acc += (x < npred) ? g_arr[x] : 0.0;
+            X = (X + acc) - (lastl < 0 ? 0.0 : cj);
+            // 2&3) market fulfilment (:536-566) on the market's node lane
+            const bool has_m = mkt >= 0 && is_node;
+            const double fill = db[(kk * RL + mk) * WAVE + q] + U;
+            const double inv = max0(X);
+            const double sale = (inv < fill) ? inv : fill;
+            X = has_m ? X - sale : X;
+            const double Sr = has_m ? sale : 0.0;
+            U = has_m ? (P.backlog ? fill - sale : 0.0) : U;
+            // 5) node profit (:578-613) in spec_core's sum orders
+            double SR = 0.0, sold = 0.0;
+#pragma unroll
+            for (int x = 0; x < SM; x++) {
+                const bool in = x < nsucc, re = skind[x] == 0;
+                SR += in ? (re ? g_sP[x] : rlp * Sr) : 0.0;
+                sold += in ? (re ? g_sR[x] : Sr) : 0.0;
+            }
+            double PC = 0.0, HCp = 0.0;
+#pragma unroll
+            for (int x = 0; x < PM; x++) PC += (x < npred) ? g_lpR[x] : 0.0;
+            const double HC_on = hj * max0(X);
+#pragma unroll
+            for (int x = 0; x < PM; x++) HCp += (x < npred) ? g_lgY[x] : 0.0;
+            const double HC = HC_on + HCp;
+            const double OC = facj ? ((vj > 0) ? oj * (sold / vj) : 0.0) : 0.0;
+            const double UP = (retj && mkt >= 0) ? 0.0 + rlb * U : 0.0;
+            const double pj = is_node ? SR - PC - OC - HC - UP : 0.0;
+            // total_profit_period: a sequential scan over the node lanes in node order
+            double tot = 0.0 + pj;
+#pragma unroll
+            for (int j = 1; j < J; j++) {
+                const double prev = row_shr1(tot);
+                tot = (l == j) ? prev + pj : tot;
+            }
+            const double rw = apow * tot;                     // :619, on lane J - 1
+            // the obs wave's record: U[t+1], X[t+1], R[t] of the links with L > 0
+            if (is_node && mkt >= 0) rb[(kk * NR + mk) * WAVE + q] = (float)U;
+            if (is_node) rb[(kk * NR + RL + l) * WAVE + q] = (float)X;
+            if (reccol >= 0) rb[(kk * NR + reccol) * WAVE + q] = (float)Rn;
+            if (valid && l == J - 1) {
+                out_store(io.rew + oi, rw);
+                out_store(io.term + oi, (uint8_t)0);
+                out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.T ? 1 : 0));
+            }
+            t += 1;
+        }
+#pragma unroll
+        for (int i = 0; i < CH; i++) acur[i] = anxt[i];
+        net_wg_sync();   // barrier c + 1: demand chunk c + 1 and record chunk c ready
+    }
+    if (valid) {
+        if (is_node) st_store(P.X + (int64_t)l * S + e, X);
+        if (is_node && mkt >= 0) st_store(P.U + (int64_t)mk * S + e, U);
+        if (is_link) st_store(P.Y + (int64_t)lk * S + e, Y);
+        // ring rows older than the episode are stored as zeros (the reference's zeroed history)
+        for (int a = 1; a <= (is_link ? Lk : 0); a++) {
+            const int row = roff + (int)((uint32_t)(t - a + 256 * Lk) % (uint32_t)Lk);
+            const double v = rg[row * QE];
+            st_store(P.Rring + (int64_t)row * S + e, (t - a >= 0) ? v : 0.0);
+        }
+    }
+}
+
 }  // namespace
 
 template <class G>
@@ -1457,6 +1904,13 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
         (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
         const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE));
         using R3 = NetRoll3<G, NET_ROLL3_CH>;
+        // small shards, open loop: the edge work of an env spread over a 16-lane row
+        if (!pol && p.cm.N <= p.cm.kn.net_rollq_max_n && !p.cm.info_demand && p.T <= NetQ<G>::AP) {
+            const dim3 gq((unsigned)((p.cm.N + NetQ<G>::QE - 1) / NetQ<G>::QE));
+            if (ph) hipLaunchKernelGGL((net_rollq_kernel<G, PhiloxGen>), gq, dim3(6 * WAVE), NetQ<G>::lds(), s, p, t_u, io);
+            else hipLaunchKernelGGL((net_rollq_kernel<G, Pcg>), gq, dim3(6 * WAVE), NetQ<G>::lds(), s, p, t_u, io);
+            return hipGetLastError();
+        }
         // the 3-role net_roll3o_kernel by default (measured on MI355X, 30-step
         // launches: 32 768 envs 69 vs 97 us, 65 536 envs 140 vs 185 us against
         // net_roll_kernel)
