@@ -5,12 +5,15 @@ Default workload (north_star target): InvManagementBacklogEnv, 4 stages,
 the C ABI (libinvsim `invsim_step`), actions pre-generated in HBM (a pool of
 distinct batches cycled per step), outputs into preallocated device buffers,
 NEXT_STEP autoreset (an episode boundary every 31 steps is part of the work).
-The step outputs land in a [32, N] slab that the HIP episode fold
-(`invsim_episode_fold`) reduces to episodic-return statistics every 32 steps
-inside the timed region; one all-reduce of them follows the region.  After
-the step region the same handle runs a timed region of fused K=30 rollouts
-(`invsim_rollout`), reported under "rollout" in the same line, and the step
-loop again as HIP-graph replays (one episode cycle per replay), under "graph".
+The step outputs land in a [128, N] slab that the HIP episode fold
+(`invsim_episode_fold_groups`) reduces to episodic-return statistics every
+128 steps inside the timed region (rollouts fold inside their kernels instead:
+the episode sink, `invsim_set_episode_sink`); one all-reduce of the statistics
+follows the region.  After the step region the same handle runs a timed region
+of fused K=30 rollouts (`invsim_rollout`), reported under "rollout" in the
+same line, and the step loop again as HIP-graph replays (one episode cycle per
+replay), under "graph".  The default line then times BASELINE configs 2, 4
+(per-GPU shard) and 5 the same way, under "configs".
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--mode step|rollout]
 
@@ -25,9 +28,12 @@ the workload's env count over the ranks instead (strong scaling).
 Prints ONE JSON line (rank 0).  `roofline.frac` = frac_kernel: algorithmic
 bytes per launch (SURVEY §8(d) B1 x N) / mean launch duration from HIP events
 on the stream the kernel runs on; `frac_wall` beside it uses the wall-clock
-`value` instead.  `cpu_baseline` = the C oracle (a single-thread port of the
-reference step, env loop OpenMP-parallel over up to 16 host cores; the
-single-thread rate beside it) timed on this host on a bounded sample.
+`value` instead; `roofline.hbm_counter` is the physical rate: PMC counter
+bytes per launch over the dominant kernel's rocprofv3 time (committed
+profiles/rNN files).  `cpu_baseline` = the C oracle (a single-thread port of
+the reference step, env loop OpenMP-parallel over up to 16 host cores; the
+single-thread rate beside it) timed on this host on a bounded sample, with the
+reference's own Python rate quoted from BASELINE.md beside it.
 """
 import argparse
 import json
@@ -248,13 +254,14 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     """Warm up, then time `steps` env.step()s of the whole batch (mode "step":
     one invsim_step each; "rollout": invsim_rollout launches of K steps;
     "policy": invsim_rollout_policy launches), with barrier + synchronize on
-    both sides and the max over ranks.  The step outputs are written into
-    [R, N] slabs that the HIP episode fold (invsim_episode_fold) reduces every
-    R steps inside the timed region, on the kernel stream between blocks
-    (--fold inline, the default; --fold side is the measured-slower side-stream
-    variant); the statistics are all-reduced once after the region.  The clock
-    stops when the kernel stream's last event completes (--stop event) or at
-    the return of torch.cuda.synchronize (--stop sync); torch.cuda.synchronize
+    both sides and the span over ranks.  The step outputs are written into
+    [R, N] slabs; the episodic-return statistics come from the episode sink in
+    the kernels (fold "sink") or from the HIP group fold
+    (invsim_episode_fold_groups) of each slab on the kernel stream between
+    blocks (fold "inline"; "side" is the measured-slower side-stream variant);
+    they are all-reduced once after the region.  The clock stops when the
+    kernel stream's last event completes (--stop spin / event) or at the
+    return of torch.cuda.synchronize (--stop sync); torch.cuda.synchronize
     closes the region either way."""
     import torch
     import invsim
@@ -268,11 +275,11 @@ def run_region(args, env, wl, mode, steps, warmup, world, dev, gen, dist):
     acts = make_actions(env, pool, K, gen) if mode != "policy" else []
     ptrs = [a.data_ptr() for a in acts]
     # slab rows = steps per fold: 128 single steps, or 4 launches of K steps.  The
-    # fold is a separate launch between blocks (~9 us of stream time each,
-    # measured), so blocks are long
+    # fold is a separate launch between blocks (17 us per 128 rows at 65 536
+    # envs, measured), so blocks are long
     LPB = 4                                         # launches per block (rollout / policy)
     R = LPB * K if K else 128
-    # two output slabs, alternating per block.  --fold inline (the default) runs
+    # two output slabs, alternating per block.  --fold inline (auto for steps) runs
     # each block's fold on the kernel stream after the block; --fold side runs it
     # on a side stream while the steps write the other slab (events order slab
     # reuse), measured slower because the fold then shares the CUs with the steps

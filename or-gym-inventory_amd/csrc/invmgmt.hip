@@ -1037,8 +1037,8 @@ struct ImLt3 {
     static constexpr int RD = IM_ROLL3_RD;                               // demand ring depth (chunks)
     static constexpr int lt(int i) { return i == 0 ? L0 : i == 1 ? L1 : L2; }
     static constexpr int W(int i) { return lt(i) > 0 ? lt(i) : 1; }      // register window length
-    static constexpr size_t lds() {
-        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8;
+    static constexpr size_t lds() {   // + the episode sink's [3][WAVE] sums (EpLaneLds)
+        return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + 3 * WAVE * 8;
     }
 };
 
@@ -1049,8 +1049,11 @@ struct ImLt3 {
 // window it already holds (plus the age-D row, wold) -- every output is
 // optional, and the evaluate_agent sums accumulate in registers (as
 // im_launch_step / im_step_regs, same order).
+// waves_per_eu(2): at most 256 registers in all, so two dynamics waves share a
+// SIMD (the policy variant sits at 256 VGPRs, and the compiler would otherwise
+// take AGPRs beyond them: one wave per SIMD, measured 104 -> 166 us)
 template <int L0, int L1, int L2, bool BACKLOG, bool POL, class RG = Pcg>
-__global__ void __launch_bounds__(2 * WAVE)
+__global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
 im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO pol) {
     using G = ImLt3<L0, L1, L2>;
     constexpr int M1 = G::M1, D = G::D, O = G::O, CH = G::CH;
@@ -1132,15 +1135,13 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO p
     double napow = P.alpha_pow[t < P.periods ? t : 0];   // alpha**t of the next step, prefetched
     int64_t dlast = 0;
     bool last_real = false;
-    // episode sink (kernels.hpp EpSink), accumulated in registers over the launch
+    // episode sink (kernels.hpp EpSink), accumulated in registers over the launch;
+    // the group's partials are read only after the loop (they would hold 8
+    // VGPRs through it: the policy kernel then needs AGPRs, one wave per SIMD)
     double *const ep_part = P.cm.ep_ret ? P.cm.ep_part + 4 * (e0 / WAVE) : nullptr;
-    EpPart epp;
-    EpLane ep;
+    EpLaneLds ep;
     bool ep_done = false;
-    if (ep_part) {
-        epp.load(ep_part);
-        ep.r = valid ? P.cm.ep_ret[e] : 0.0;
-    }
+    if (ep_part) ep.init(reinterpret_cast<double *>(dbuf + G::RD * CH * WAVE), lane, valid ? P.cm.ep_ret[e] : 0.0);
     wg_lds_sync();   // barrier 0: chunk 0 ready
     for (int c = 0; c < nch; c++) {
         const int64_t *db = dbuf + (c % G::RD) * CH * WAVE;
@@ -1348,7 +1349,11 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO p
         }
         if (ep_part) P.cm.ep_ret[e] = ep.r;
     }
-    if (ep_part) epp.flush(ep_part, ep, __ballot(ep_done) != 0, lane);
+    if (ep_part) {
+        EpPart epp;
+        epp.load(ep_part);
+        epp.flush(ep_part, ep.get(), __ballot(ep_done) != 0, lane);
+    }
 }
 
 // im_roll3_kernel with the observation work moved to a third wave (for small
@@ -1393,7 +1398,7 @@ struct ImLt3o : ImLt3<L0, L1, L2> {
     static constexpr size_t actl_n(bool pol) { return (IM_ROLL3O_STAGE && !pol) ? (size_t)2 * CH * 2 * M1 * WAVE : 0; }
     static constexpr size_t lds(bool pol) {
         return (size_t)WAVE * O * 8 + RHS_LDS_MAX * 8 + (size_t)RD * CH * WAVE * 8 + (size_t)2 * CH * M1 * WAVE * 8 +
-               abuf_n(pol) * 8 + actl_n(pol) * 4 + IM_AP_LDS * 8;
+               abuf_n(pol) * 8 + actl_n(pol) * 4 + IM_AP_LDS * 8 + 3 * WAVE * 8;   // + EpLaneLds sums
     }
 };
 
@@ -1585,15 +1590,13 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
     for (int i = 0; i < M1; i++) nact[i] = (POL || STAGED) ? 0 : io.act[el * M1 + i];
     int64_t dlast = 0;
     bool last_real = false;
-    // episode sink (kernels.hpp EpSink), accumulated in registers over the launch
+    // episode sink (kernels.hpp EpSink), accumulated in registers over the launch;
+    // the group's partials are read only after the loop (they would hold 8
+    // VGPRs through it: the policy kernel then needs AGPRs, one wave per SIMD)
     double *const ep_part = P.cm.ep_ret ? P.cm.ep_part + 4 * (e0 / WAVE) : nullptr;
-    EpPart epp;
-    EpLane ep;
+    EpLaneLds ep;
     bool ep_done = false;
-    if (ep_part) {
-        epp.load(ep_part);
-        ep.r = valid ? P.cm.ep_ret[e] : 0.0;
-    }
+    if (ep_part) ep.init(reinterpret_cast<double *>(ap_l + IM_AP_LDS), lane, valid ? P.cm.ep_ret[e] : 0.0);
     wg_lds_sync();   // barrier 0: demand chunk 0 (and its actions when staged, alpha**t) ready
     for (int c = 0; c < nch; c++) {
         const int64_t *db = dbuf + (c % G::RD) * CH * WAVE;
@@ -1770,7 +1773,11 @@ im_roll3o_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO 
         }
         if (ep_part) P.cm.ep_ret[e] = ep.r;
     }
-    if (ep_part) epp.flush(ep_part, ep, __ballot(ep_done) != 0, lane);
+    if (ep_part) {
+        EpPart epp;
+        epp.load(ep_part);
+        epp.flush(ep_part, ep.get(), __ballot(ep_done) != 0, lane);
+    }
     TWAIT();
     TPROBE_W(6);
 }

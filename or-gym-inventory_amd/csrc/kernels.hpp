@@ -197,6 +197,43 @@ struct EpLane {
     }
 };
 
+// EpLane for the rollout kernels: the running return and the reward sum in
+// registers, the three sums that change only at an episode's end in LDS (the
+// owning lane's column of a [3][WAVE] block), so the sink holds 4 VGPRs
+// through the launch's loop (the 2-role policy kernel sits at 256).  The same
+// operations in the same order as EpLane.
+struct EpLaneLds {
+    static constexpr int W = 64;   // lanes (the column stride)
+    double r = 0.0, all = 0.0;
+    double *sl;
+    __device__ __forceinline__ void init(double *base, int lane, double r0) {
+        sl = base + lane;
+        sl[0] = 0.0;
+        sl[W] = 0.0;
+        sl[2 * W] = 0.0;
+        r = r0;
+    }
+    __device__ __forceinline__ void add(double rew, bool done) {
+        r += rew;
+        all += rew;
+        if (done) {
+            sl[0] += r;
+            sl[W] += r * r;
+            sl[2 * W] += 1.0;
+            r = 0.0;
+        }
+    }
+    __device__ __forceinline__ EpLane get() const {
+        EpLane a;
+        a.r = r;
+        a.all = all;
+        a.s = sl[0];
+        a.s2 = sl[W];
+        a.c = sl[2 * W];
+        return a;
+    }
+};
+
 // The group's partials, loaded early (before the launch's other work ends) so
 // the read-modify-write at the end waits for nothing
 struct EpPart {
