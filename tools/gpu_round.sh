@@ -18,8 +18,10 @@ run() {
     rc=$?
     if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $*" >&2; exit $rc; fi
 }
-WLS="invmgmt_backlog invmgmt_lostsales newsvendor net_backlog"
-B="--no-cpu-baseline --no-rollout-line --no-graph-line"
+WLS=${WLS:-"invmgmt_backlog invmgmt_lostsales newsvendor net_backlog"}
+# --no-config-lines: the default workload's line would also time configs 2, 4, 5 in the
+# same process, and their kernels would enter the traces and counter passes
+B="--no-cpu-baseline --no-rollout-line --no-graph-line --no-config-lines"
 for part in $PARTS; do
   case $part in
   tests)
