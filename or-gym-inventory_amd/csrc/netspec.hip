@@ -105,13 +105,12 @@ __device__ __forceinline__ void net_demand_loop(RG &g, const PtrsConst (&pc)[G::
 // row into orow (LDS).  Returns the reward; Rn receives R[t] (the fulfilled
 // orders) per link.
 //
-// spec_core: the step without the observation, given each link's age-L window
-// entry wa[k] = R[t - L_k] (the arrival; unused for L == 0).
+// spec_flow: phases 0-3 of the step (orders, pipeline, arrivals, market), the
+// state update without the profit; Sr receives the market sales.
 template <class G, class RG = Pcg>
-__device__ __forceinline__ double spec_core(const NetParams &P, double apow, NetSt<G, RG> &s,
-                                            const float (&act)[G::E], const double (&Dd)[G::RL],
-                                            const double (&wa)[G::E], double (&Rn)[G::E], double *met,
-                                            double *irec) {
+__device__ __forceinline__ void spec_flow(const NetParams &P, NetSt<G, RG> &s, const float (&act)[G::E],
+                                          const double (&Dd)[G::RL], const double (&wa)[G::E], double (&Rn)[G::E],
+                                          double (&Sr)[G::RL]) {
     double cons[G::J];
 #pragma unroll
     for (int j = 0; j < G::J; j++) cons[j] = 0.0;
@@ -153,7 +152,6 @@ __device__ __forceinline__ double spec_core(const NetParams &P, double apow, Net
         s.X[j] = (s.X[j] + acc) - cons[j];
     }
     // 2&3) market fulfilment in retail-link edge order (:536-566)
-    double Sr[G::RL];
 #pragma unroll
     for (int r = 0; r < G::RL; r++) {
         const double fill = Dd[r] + s.U[r];
@@ -164,6 +162,59 @@ __device__ __forceinline__ double spec_core(const NetParams &P, double apow, Net
         Sr[r] = sale;
         s.U[r] = P.backlog ? fill - sale : 0.0;
     }
+}
+
+// spec_profit: phase 5, the period's total profit over the main nodes
+// (:578-613, Python sum() order = adjacency order) from R[t], the market sales,
+// X[t+1], Y[t+1] and U[t+1]; pj (nullable) receives each node's profit.
+template <class G>
+__device__ __forceinline__ double spec_profit(const double (&Rn)[G::E], const double (&Sr)[G::RL],
+                                              const double (&X)[G::J], const double (&Y)[G::E],
+                                              const double (&U)[G::RL], double *pjo) {
+    double total = 0.0;
+#pragma unroll
+    for (int j = 0; j < G::J; j++) {
+        double SR = 0.0, sold = 0.0;
+#pragma unroll
+        for (int q = G::succ_ptr[j]; q < G::succ_ptr[j + 1]; q++) {
+            const int idx = G::succ_idx[q];
+            const bool re = G::succ_kind[q] == 0;
+            const double sv = re ? Rn[idx < G::E ? idx : 0] : Sr[idx < G::RL ? idx : 0];
+            SR += (re ? G::lp[idx < G::E ? idx : 0] : G::rl_p[idx < G::RL ? idx : 0]) * sv;
+            sold += sv;
+        }
+        double PC = 0.0, HCp = 0.0;
+#pragma unroll
+        for (int q = G::pred_ptr[j]; q < G::pred_ptr[j + 1]; q++) PC += G::lp[G::pred_idx[q]] * Rn[G::pred_idx[q]];
+        const double HC_on = G::h[j] * max0(X[j]);
+#pragma unroll
+        for (int q = G::pred_ptr[j]; q < G::pred_ptr[j + 1]; q++) HCp += G::lg[G::pred_idx[q]] * max0(Y[G::pred_idx[q]]);
+        const double HC = HC_on + HCp;
+        double OC = 0.0;
+        if (G::is_factory[j]) OC = (G::v[j] > 0) ? G::o[j] * (sold / G::v[j]) : 0.0;
+        double UP = 0.0;
+        if (G::is_retail[j]) {
+#pragma unroll
+            for (int q = G::succ_ptr[j]; q < G::succ_ptr[j + 1]; q++)
+                if (G::succ_kind[q] == 1) UP += G::rl_b[G::succ_idx[q] < G::RL ? G::succ_idx[q] : 0] *
+                                                U[G::succ_idx[q] < G::RL ? G::succ_idx[q] : 0];
+        }
+        const double pj = SR - PC - OC - HC - UP;
+        if (pjo) pjo[j] = pj;
+        total += pj;
+    }
+    return total;
+}
+
+// spec_core: the step without the observation, given each link's age-L window
+// entry wa[k] = R[t - L_k] (the arrival; unused for L == 0).
+template <class G, class RG = Pcg>
+__device__ __forceinline__ double spec_core(const NetParams &P, double apow, NetSt<G, RG> &s,
+                                            const float (&act)[G::E], const double (&Dd)[G::RL],
+                                            const double (&wa)[G::E], double (&Rn)[G::E], double *met,
+                                            double *irec) {
+    double Sr[G::RL];
+    spec_flow<G>(P, s, act, Dd, wa, Rn, Sr);
     if (irec) {  // step record: S[t, retail], U[t+1, retail], X[t+1, main] (network_management.py:536-571)
 #pragma unroll
         for (int r = 0; r < G::RL; r++) {
@@ -188,39 +239,7 @@ __device__ __forceinline__ double spec_core(const NetParams &P, double apow, Net
 #pragma unroll
         for (int j = 0; j < G::J; j++) met[5 + j] += s.X[j];   // X[t+1, main nodes] per node
     }
-    // 5) profit per main node (:578-613), Python sum() order = adjacency order
-    double total = 0.0;
-#pragma unroll
-    for (int j = 0; j < G::J; j++) {
-        double SR = 0.0, sold = 0.0;
-#pragma unroll
-        for (int q = G::succ_ptr[j]; q < G::succ_ptr[j + 1]; q++) {
-            const int idx = G::succ_idx[q];
-            const bool re = G::succ_kind[q] == 0;
-            const double sv = re ? Rn[idx < G::E ? idx : 0] : Sr[idx < G::RL ? idx : 0];
-            SR += (re ? G::lp[idx < G::E ? idx : 0] : G::rl_p[idx < G::RL ? idx : 0]) * sv;
-            sold += sv;
-        }
-        double PC = 0.0, HCp = 0.0;
-#pragma unroll
-        for (int q = G::pred_ptr[j]; q < G::pred_ptr[j + 1]; q++) PC += G::lp[G::pred_idx[q]] * Rn[G::pred_idx[q]];
-        const double HC_on = G::h[j] * max0(s.X[j]);
-#pragma unroll
-        for (int q = G::pred_ptr[j]; q < G::pred_ptr[j + 1]; q++) HCp += G::lg[G::pred_idx[q]] * max0(s.Y[G::pred_idx[q]]);
-        const double HC = HC_on + HCp;
-        double OC = 0.0;
-        if (G::is_factory[j]) OC = (G::v[j] > 0) ? G::o[j] * (sold / G::v[j]) : 0.0;
-        double UP = 0.0;
-        if (G::is_retail[j]) {
-#pragma unroll
-            for (int q = G::succ_ptr[j]; q < G::succ_ptr[j + 1]; q++)
-                if (G::succ_kind[q] == 1) UP += G::rl_b[G::succ_idx[q] < G::RL ? G::succ_idx[q] : 0] *
-                                                s.U[G::succ_idx[q] < G::RL ? G::succ_idx[q] : 0];
-        }
-        const double pj = SR - PC - OC - HC - UP;
-        if (irec) irec[2 * G::RL + G::J + 2 * G::E + j] = pj;   // P[t, node]
-        total += pj;
-    }
+    const double total = spec_profit<G>(Rn, Sr, s.X, s.Y, s.U, irec ? irec + 2 * G::RL + G::J + 2 * G::E : nullptr);
     return apow * total;                                       // :619
 }
 
@@ -1364,6 +1383,288 @@ net_roll3o_kernel(NetParams P, int t_start, StepIO<float, float> io, PolicyIO po
     }
 }
 
+// ---------------------------------------------------------------- 4 roles
+// net_roll3o_kernel with the period's profit on a wave of its own, for batches
+// up to 256 workgroups (one per CU: the record below takes the LDS).  At small
+// shards every role has a SIMD to itself and the dynamics wave's instruction
+// chain is the step time: ~425 instructions, 240 of them f64, about half of
+// those the per-node profit sums (spec_profit).  One 256-thread workgroup per
+// 64 envs:
+//   wave 0 (demand)   as net_roll3o_kernel's
+//   wave 1 (flow)     spec_flow (orders, pipeline, arrivals, market) with the
+//                     order rings in LDS; hands R[t], the market sales,
+//                     X[t+1], Y[t+1] and U[t+1] of every step to waves 2 and 3
+//                     in the f64 record rec4[c & 1]
+//   wave 2 (obs)      as net_roll3o_kernel's, from rec4 (rounded to f32)
+//   wave 3 (profit)   spec_profit and apow * total from rec4, and the reward,
+//                     terminated and truncated outputs, one chunk behind the
+//                     flow wave
+// Same arithmetic, in the same order, as net_spec_kernel.
+template <class G>
+struct NetRoll4 {
+    static constexpr int CH = NET_ROLL3_CH, RD = NET_ROLL3_RD;
+    static constexpr int NR4 = 2 * G::E + 2 * G::RL + G::J;            // rec4 columns: R, Sr, X, Y, U
+    static constexpr int AP = 256;                                     // alpha**t in LDS (T <= AP)
+    static constexpr size_t tile_bytes() { return (size_t)((EPW * G::O + 3) / 4) * 4 * sizeof(float); }
+    static constexpr size_t rhs_bytes() { return (size_t)G::RL * RHS_LDS_MAX * sizeof(double); }
+    static constexpr size_t dbuf_bytes() { return (size_t)RD * CH * G::RL * WAVE * sizeof(double); }
+    static constexpr size_t ring_bytes() { return (size_t)(G::sumL > 0 ? G::sumL : 1) * WAVE * sizeof(double); }
+    static constexpr size_t rec_bytes() { return 2 * (size_t)CH * NR4 * WAVE * sizeof(double); }
+    static constexpr size_t lds() {
+        return tile_bytes() + rhs_bytes() + dbuf_bytes() + ring_bytes() + rec_bytes() + AP * sizeof(double);
+    }
+    // rec4 column of R[t] link k, the sales of market r, X[t+1] node j, Y[t+1] link k, U[t+1] market r
+    static constexpr int cR(int k) { return k; }
+    static constexpr int cS(int r) { return G::E + r; }
+    static constexpr int cX(int j) { return G::E + G::RL + j; }
+    static constexpr int cY(int k) { return G::E + G::RL + G::J + k; }
+    static constexpr int cU(int r) { return 2 * G::E + G::RL + G::J + r; }
+};
+
+template <class G, class RG = Pcg>
+__global__ void __launch_bounds__(4 * WAVE)
+net_roll4_kernel(NetParams P, int t_start, StepIO<float, float> io) {
+    using R4 = NetRoll4<G>;
+    using LP = NetLpos<G>;
+    constexpr int O = G::O, CH = R4::CH, RD = R4::RD, RL = G::RL, NR4 = R4::NR4, E = G::E, J = G::J;
+    constexpr int TILE_IT = (EPW * O * 4 + 16 * WAVE - 1) / (16 * WAVE);
+    extern __shared__ __attribute__((aligned(16))) float n4_lds[];
+    char *lb = reinterpret_cast<char *>(n4_lds);
+    float *tile = n4_lds;
+    double *rhs_l = reinterpret_cast<double *>(lb + R4::tile_bytes());
+    double *dbuf = reinterpret_cast<double *>(lb + R4::tile_bytes() + R4::rhs_bytes());     // [RD * CH][RL][WAVE]
+    double *ring = reinterpret_cast<double *>(lb + R4::tile_bytes() + R4::rhs_bytes() + R4::dbuf_bytes());
+    double *rec = reinterpret_cast<double *>(lb + R4::tile_bytes() + R4::rhs_bytes() + R4::dbuf_bytes() +
+                                             R4::ring_bytes());                              // [2][CH][NR4][WAVE]
+    double *ap_l = rec + 2 * CH * NR4 * WAVE;                                                // alpha**t, t < T
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int role = threadIdx.x / WAVE;
+    const int64_t N = P.cm.N;
+    const int64_t S = P.cm.Npad;
+    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e = e0 + lane;
+    const bool valid = e < N;
+    const int64_t el = valid ? e : N - 1;       // padded lanes: the last env's data, never stored
+    const int nvalid = (int)((N - e0) < WAVE ? (N - e0) : WAVE);
+    const int K = io.K;
+    const int nch = (K + CH - 1) / CH;
+    if (role == 0) {   // ---- demand wave
+        PtrsConst pc[RL];
+#pragma unroll
+        for (int r = 0; r < RL; r++) pc[r] = P.rl_pc[r];
+        constexpr int NT = RHS_LDS_MAX / WAVE;
+        double tv[RL][NT];
+#pragma unroll
+        for (int r = 0; r < RL; r++) {
+            const int qm = pc[r].nk > 0 ? pc[r].nk - 1 : 0;
+            const double *src = pc[r].nk > 0 ? P.rhs + pc[r].toff : P.alpha_pow;   // any valid pointer
+#pragma unroll
+            for (int u = 0; u < NT; u++) tv[r][u] = src[min(lane + u * WAVE, qm)];
+        }
+        RG g;
+        P.cm.rng.load(el, g);
+        for (int x = lane; x < P.T; x += WAVE) ap_l[x] = P.alpha_pow[x];   // before barrier 0
+#pragma unroll
+        for (int r = 0; r < RL; r++)
+#pragma unroll
+            for (int u = 0; u < NT; u++) rhs_l[r * RHS_LDS_MAX + lane + u * WAVE] = tv[r][u];
+        wave_lds_sync();
+        net_demand_loop<G, CH, RD>(g, pc, rhs_l, dbuf, lane, K, nch + 1, t_start, P.T, P.cm.ph_step);
+        if (valid) P.cm.rng.store_state(e, g);
+        return;
+    }
+    if (role == 2) {   // ---- obs wave
+        float *trow = tile + lane * O;
+        int t = t_start;
+        float wf[LP::sumL1() > 0 ? LP::sumL1() : 1];
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+            if (G::L[k] <= 1) continue;
+#pragma unroll
+            for (int a = 1; a < G::L[k]; a++) {
+                const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+                const double v = P.Rring[(int64_t)row * S + el];
+                wf[LP::woff(k) + a - 1] = (t - a >= 0) ? (float)v : 0.f;
+            }
+        }
+        net_wg_sync();   // barrier 0
+        for (int c = 0; c < nch; c++) {
+            net_wg_sync();   // barrier c + 1: record chunk c ready
+            const double *rb = rec + (c & 1) * CH * NR4 * WAVE;
+            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+                const int k = c * CH + kk;
+                if (t >= P.T) {                    // NEXT_STEP autoreset: [0, I0, 0 ...] (:301-332)
+#pragma unroll
+                    for (int r = 0; r < RL; r++) trow[r] = 0.f;
+#pragma unroll
+                    for (int j = 0; j < J; j++) trow[RL + j] = (float)G::I0[j];
+#pragma unroll
+                    for (int q = 0; q < G::sumL; q++) trow[RL + J + q] = 0.f;
+#pragma unroll
+                    for (int q = 0; q < LP::sumL1(); q++) wf[q] = 0.f;
+                    t = 0;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < RL; r++) trow[r] = (float)rb[(kk * NR4 + R4::cU(r)) * WAVE + lane];
+#pragma unroll
+                    for (int j = 0; j < J; j++) trow[RL + j] = (float)rb[(kk * NR4 + R4::cX(j)) * WAVE + lane];
+#pragma unroll
+                    for (int kl = 0; kl < E; kl++) {
+                        if (G::L[kl] == 0) continue;
+                        const float rn = (float)rb[(kk * NR4 + R4::cR(kl)) * WAVE + lane];
+#pragma unroll
+                        for (int p = 0; p + 1 < G::L[kl]; p++)
+                            trow[G::win_off[kl] + p] = wf[LP::woff(kl) + (G::L[kl] - 1 - p) - 1];
+                        trow[G::win_off[kl] + G::L[kl] - 1] = rn;
+#pragma unroll
+                        for (int a = G::L[kl] - 1; a >= 2; a--) wf[LP::woff(kl) + a - 1] = wf[LP::woff(kl) + a - 2];
+                        if (G::L[kl] > 1) wf[LP::woff(kl)] = rn;
+                    }
+                    t += 1;
+                }
+                wave_lds_sync();
+                store_tile<TILE_IT>(tile, io.obs + ((int64_t)k * N + e0) * O, (int64_t)nvalid * O, lane);
+                wave_lds_sync();
+            }
+        }
+        return;
+    }
+    if (role == 3) {   // ---- profit wave
+        int t = t_start;
+        net_wg_sync();   // barrier 0
+        for (int c = 0; c < nch; c++) {
+            net_wg_sync();   // barrier c + 1: record chunk c ready
+            const double *rb = rec + (c & 1) * CH * NR4 * WAVE;
+            for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+                const int64_t oi = (int64_t)(c * CH + kk) * N + e;
+                if (t >= P.T) {                    // the NEXT_STEP reset step: reward 0, no flag
+                    if (valid) {
+                        out_store(io.rew + oi, 0.0);
+                        out_store(io.term + oi, (uint8_t)0);
+                        out_store(io.trunc + oi, (uint8_t)0);
+                    }
+                    t = 0;
+                    continue;
+                }
+                double Rn[E], Sr[RL], X[J], Y[E], U[RL];
+#pragma unroll
+                for (int k = 0; k < E; k++) Rn[k] = rb[(kk * NR4 + R4::cR(k)) * WAVE + lane];
+#pragma unroll
+                for (int r = 0; r < RL; r++) Sr[r] = rb[(kk * NR4 + R4::cS(r)) * WAVE + lane];
+#pragma unroll
+                for (int j = 0; j < J; j++) X[j] = rb[(kk * NR4 + R4::cX(j)) * WAVE + lane];
+#pragma unroll
+                for (int k = 0; k < E; k++) Y[k] = rb[(kk * NR4 + R4::cY(k)) * WAVE + lane];
+#pragma unroll
+                for (int r = 0; r < RL; r++) U[r] = rb[(kk * NR4 + R4::cU(r)) * WAVE + lane];
+                const double rw = ap_l[t] * spec_profit<G>(Rn, Sr, X, Y, U, nullptr);   // :619
+                if (valid) {
+                    out_store(io.rew + oi, rw);
+                    out_store(io.term + oi, (uint8_t)0);
+                    out_store(io.trunc + oi, (uint8_t)(t + 1 >= P.T ? 1 : 0));
+                }
+                t += 1;
+            }
+        }
+        return;
+    }
+    // ---- flow wave
+    double *rg = ring + lane;                   // [sumL][WAVE]: R[t'] of link k at row ring_off[k] + t' mod L
+    int t = t_start;
+    NetSt<G> st;
+#pragma unroll
+    for (int j = 0; j < J; j++) st.X[j] = P.X[j * S + el];
+#pragma unroll
+    for (int r = 0; r < RL; r++) st.U[r] = P.U[r * S + el];
+#pragma unroll
+    for (int k = 0; k < E; k++) st.Y[k] = P.Y[k * S + el];
+    {
+        double rv[G::sumL > 0 ? G::sumL : 1];
+#pragma unroll
+        for (int q = 0; q < G::sumL; q++) rv[q] = P.Rring[(int64_t)q * S + el];
+#pragma unroll
+        for (int q = 0; q < G::sumL; q++) rg[q * WAVE] = rv[q];
+    }
+    float nact[E];
+#pragma unroll
+    for (int k = 0; k < E; k++) nact[k] = io.act[el * E + k];
+    double Rn[E];
+    net_wg_sync();   // barrier 0: demand chunk 0 ready
+    for (int c = 0; c < nch; c++) {
+        const double *db = dbuf + (c % RD) * CH * RL * WAVE;
+        double *rb = rec + (c & 1) * CH * NR4 * WAVE;
+        for (int kk = 0; kk < CH && c * CH + kk < K; kk++) {
+            const int k = c * CH + kk;
+            float act[E];
+#pragma unroll
+            for (int q = 0; q < E; q++) act[q] = nact[q];
+            if (k + 1 < K) {                                    // the next step's actions
+#pragma unroll
+                for (int q = 0; q < E; q++) nact[q] = io.act[((int64_t)(k + 1) * N + el) * E + q];
+            }
+            if (t >= P.T) {                                     // NEXT_STEP autoreset (:301-332)
+#pragma unroll
+                for (int j = 0; j < J; j++) st.X[j] = G::I0[j];
+#pragma unroll
+                for (int r = 0; r < RL; r++) st.U[r] = 0.0;
+#pragma unroll
+                for (int q = 0; q < E; q++) st.Y[q] = 0.0;
+                t = 0;
+            } else {
+                double Dd[RL], wa[E], Sr[RL];
+#pragma unroll
+                for (int r = 0; r < RL; r++) Dd[r] = db[(kk * RL + r) * WAVE + lane];
+#pragma unroll
+                for (int q = 0; q < E; q++) {                  // arrival R[t - L] (zero before the episode)
+                    if (G::L[q] == 0) {
+                        wa[q] = 0.0;
+                        continue;
+                    }
+                    const double v = rg[(G::ring_off[q] + (int)((uint32_t)t % (uint32_t)G::L[q])) * WAVE];
+                    wa[q] = (t >= G::L[q]) ? v : 0.0;
+                }
+                spec_flow<G>(P, st, act, Dd, wa, Rn, Sr);
+#pragma unroll
+                for (int q = 0; q < E; q++)
+                    if (G::L[q] > 0) rg[(G::ring_off[q] + (int)((uint32_t)t % (uint32_t)G::L[q])) * WAVE] = Rn[q];
+#pragma unroll
+                for (int q = 0; q < E; q++) {
+                    rb[(kk * NR4 + R4::cR(q)) * WAVE + lane] = Rn[q];
+                    rb[(kk * NR4 + R4::cY(q)) * WAVE + lane] = st.Y[q];
+                }
+#pragma unroll
+                for (int r = 0; r < RL; r++) {
+                    rb[(kk * NR4 + R4::cS(r)) * WAVE + lane] = Sr[r];
+                    rb[(kk * NR4 + R4::cU(r)) * WAVE + lane] = st.U[r];
+                }
+#pragma unroll
+                for (int j = 0; j < J; j++) rb[(kk * NR4 + R4::cX(j)) * WAVE + lane] = st.X[j];
+                t += 1;
+            }
+        }
+        net_wg_sync();   // barrier c + 1: demand chunk c + 1 and record chunk c ready
+    }
+    if (valid) {
+#pragma unroll
+        for (int j = 0; j < J; j++) st_store(P.X + j * S + e, st.X[j]);
+#pragma unroll
+        for (int r = 0; r < RL; r++) st_store(P.U + r * S + e, st.U[r]);
+#pragma unroll
+        for (int k = 0; k < E; k++) st_store(P.Y + k * S + e, st.Y[k]);
+        // ring rows older than the episode are stored as zeros (the reference's zeroed history)
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+            if (G::L[k] == 0) continue;
+#pragma unroll
+            for (int a = 1; a <= G::L[k]; a++) {
+                const int row = G::ring_off[k] + (int)((uint32_t)(t - a + 256 * G::L[k]) % (uint32_t)G::L[k]);
+                const double v = rg[row * WAVE];
+                st_store(P.Rring + (int64_t)row * S + e, (t - a >= 0) ? v : 0.0);
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- small shards
 // The K-step rollout for small per-GPU shards (config 5 split over 8 GPUs:
 // 4 096 envs per rank).  There the 3-role kernel runs one dynamics wave per
@@ -1904,6 +2205,13 @@ static hipError_t spec_launch(const NetParams &p, int t_u, const PolicyIO *pol, 
         (p.cm.autoreset == AR_NEXT_STEP || (p.cm.autoreset == AR_DISABLED && t_u + io.K <= p.T))) {
         const dim3 gr((unsigned)((p.cm.N + WAVE - 1) / WAVE));
         using R3 = NetRoll3<G, NET_ROLL3_CH>;
+        // small batches, open loop: the profit on a fourth wave (one workgroup per CU)
+        if (!pol && p.cm.N <= p.cm.kn.net_roll4_max_n && !p.cm.info_demand && p.T <= NetRoll4<G>::AP &&
+            p.cm.N > p.cm.kn.net_rollq_max_n) {
+            if (ph) hipLaunchKernelGGL((net_roll4_kernel<G, PhiloxGen>), gr, dim3(4 * WAVE), NetRoll4<G>::lds(), s, p, t_u, io);
+            else hipLaunchKernelGGL((net_roll4_kernel<G, Pcg>), gr, dim3(4 * WAVE), NetRoll4<G>::lds(), s, p, t_u, io);
+            return hipGetLastError();
+        }
         // small shards, open loop: the edge work of an env spread over a 16-lane row
         if (!pol && p.cm.N <= p.cm.kn.net_rollq_max_n && !p.cm.info_demand && p.T <= NetQ<G>::AP) {
             const dim3 gq((unsigned)((p.cm.N + NetQ<G>::QE - 1) / NetQ<G>::QE));

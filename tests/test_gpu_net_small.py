@@ -1,14 +1,14 @@
 """NetInvMgmt rollouts for small per-GPU shards (SURVEY row h*, VERDICT r05
-item 3): net_rollq_kernel spreads one env's edge work over a 16-lane row
-(clamp-scan over each supplier's links, row gathers for the per-node sums,
-a node-order scan for the period profit; netspec.hip).  Bar: bit-identical
-to the one-env-per-lane net_roll3o_kernel (INVSIM_NET_ROLLQ_MAX_N=0) and to
-the C oracle stepping the same seeds (network_management.py:436-635)."""
+item 3): net_roll4_kernel puts the period profit on a wave of its own (the
+default up to 16 384 envs), and net_rollq_kernel (opt-in) spreads one env's
+edge work over a 16-lane row (clamp-scan over each supplier's links, row
+gathers for the per-node sums, a node-order scan for the period profit;
+netspec.hip).  Bar: bit-identical to the one-env-per-lane 3-role
+net_roll3o_kernel (INVSIM_NET_ROLL4_MAX_N=0 / INVSIM_NET_ROLLQ_MAX_N=0) and
+to the C oracle stepping the same seeds (network_management.py:436-635)."""
 import numpy as np
 import pytest
 import torch
-
-from conftest import knob_envs
 
 pytestmark = pytest.mark.gpu
 
@@ -21,7 +21,7 @@ def _eq_bits(a, b):
     return np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("graph,backlog,n,periods,mode,stream", [
+CASES = [
     ("default", True, 4096, 30, "next_step", "numpy"),     # config 5 over 8 GPUs: 4 096 envs per rank
     ("default", True, 4099, 30, "next_step", "numpy"),     # a partial 16-env workgroup
     ("default", False, 8192, 30, "next_step", "numpy"),
@@ -30,15 +30,33 @@ def _eq_bits(a, b):
     ("custom", True, 2000, 30, "next_step", "numpy"),      # three markets, three links on one supplier
     ("custom", False, 777, 3, "next_step", "numpy"),
     ("default", True, 4096, 30, "next_step", "philox"),
-])
-def test_rollq_equals_roll3o(gpu, monkeypatch, graph, backlog, n, periods, mode, stream):
+]
+
+
+def _pair(gpu, monkeypatch, kernel, graph, backlog, n, periods, mode, stream):
+    """(env on `kernel`, env on net_roll3o_kernel) with the same configuration"""
     import invsim
     from invsim.topology import custom_graph, default_graph
     mk_g = default_graph if graph == "default" else custom_graph
-    envs = knob_envs(monkeypatch, "INVSIM_NET_ROLLQ_MAX_N", ("100000", "0"),
-                     lambda: invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), backlog=backlog,
-                                                        num_periods=periods, autoreset_mode=mode,
-                                                        demand_stream=stream))
+    mk = (lambda: invsim.NetInvMgmtMasterEnv(n, device=gpu, graph=mk_g(), backlog=backlog, num_periods=periods,
+                                             autoreset_mode=mode, demand_stream=stream))
+    monkeypatch.setenv("INVSIM_NET_ROLL4_MAX_N", "0")
+    monkeypatch.setenv("INVSIM_NET_ROLLQ_MAX_N", "0")
+    ref = mk()
+    if kernel == "rollq":
+        monkeypatch.setenv("INVSIM_NET_ROLLQ_MAX_N", "100000")
+    else:
+        monkeypatch.setenv("INVSIM_NET_ROLL4_MAX_N", "100000")
+    env = mk()
+    monkeypatch.delenv("INVSIM_NET_ROLL4_MAX_N")
+    monkeypatch.delenv("INVSIM_NET_ROLLQ_MAX_N")
+    return [env, ref]
+
+
+@pytest.mark.parametrize("kernel", ["roll4", "rollq"])
+@pytest.mark.parametrize("graph,backlog,n,periods,mode,stream", CASES)
+def test_small_shard_rollout_equals_roll3o(gpu, monkeypatch, kernel, graph, backlog, n, periods, mode, stream):
+    envs = _pair(gpu, monkeypatch, kernel, graph, backlog, n, periods, mode, stream)
     for env in envs:
         env.reset(seed=31)
     A = envs[0].action_dim
@@ -61,17 +79,19 @@ def test_rollq_equals_roll3o(gpu, monkeypatch, graph, backlog, n, periods, mode,
             assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("kernel", ["roll4", "rollq"])
 @pytest.mark.parametrize("graph", ["default", "custom"])
-def test_rollq_vs_oracle(gpu, oracle, monkeypatch, graph):
+def test_small_shard_rollout_vs_oracle(gpu, oracle, monkeypatch, kernel, graph):
     """4 096 envs (one rank's shard of config 5 over 8 GPUs): a 61-step fused
     rollout across the NEXT_STEP reset, step by step against the oracle."""
     import invsim
     from invsim.topology import custom_graph, default_graph
     n, T, K = 4096, 30, 61
     g = default_graph() if graph == "default" else custom_graph()
-    monkeypatch.setenv("INVSIM_NET_ROLLQ_MAX_N", "100000")   # net_rollq_kernel (opt-in)
-    env = invsim.NetInvMgmtBacklogEnv(n, device=gpu, graph=g)
-    monkeypatch.delenv("INVSIM_NET_ROLLQ_MAX_N")
+    if kernel == "rollq":
+        monkeypatch.setenv("INVSIM_NET_ROLLQ_MAX_N", "100000")   # net_rollq_kernel (opt-in)
+    env = invsim.NetInvMgmtBacklogEnv(n, device=gpu, graph=g)   # net_roll4_kernel by default at this size
+    monkeypatch.delenv("INVSIM_NET_ROLLQ_MAX_N", raising=False)
     orc = oracle.OracleNet(n, graph=g)
     orc.seed(range(500, 500 + n))
     e_obs = orc.reset()
