@@ -97,3 +97,38 @@ def test_span_single_process():
         def is_initialized():
             return False
     assert bench._span(1.0, 3.5, None, NoDist) == 2.5
+
+
+def test_fold_mode_auto():
+    """--fold auto: the in-kernel episode sink for InvMgmt rollouts (and policy
+    rollouts), the block fold for single steps and for the other families
+    (DESIGN §4 "Round 6: the episode sink")."""
+    import types
+    import bench
+    from invsim import _capi
+
+    def env(fam):
+        return types.SimpleNamespace(family=fam)
+    a = types.SimpleNamespace(fold="auto")
+    assert bench.fold_mode(a, env(_capi.INVSIM_INVMGMT), "rollout") == "sink"
+    assert bench.fold_mode(a, env(_capi.INVSIM_INVMGMT), "policy") == "sink"
+    assert bench.fold_mode(a, env(_capi.INVSIM_INVMGMT), "step") == "inline"
+    for fam in (_capi.INVSIM_NEWSVENDOR, _capi.INVSIM_NETINVMGMT):
+        assert bench.fold_mode(a, env(fam), "rollout") == "inline"
+    for f in ("sink", "side", "inline", "none"):
+        assert bench.fold_mode(types.SimpleNamespace(fold=f), env(_capi.INVSIM_NEWSVENDOR), "step") == f
+
+
+def test_episode_stats_host_partials():
+    """host EpisodeStats: one partial row; acc is its column sum; reset_acc
+    keeps the running returns"""
+    from invsim.distributed import EpisodeStats
+    st = EpisodeStats(5, "cpu")
+    assert tuple(st.part.shape) == (1, 4)
+    rew = torch.tensor([[1.0, 2.0, 3.0, 4.0, 5.0], [1.0, 1.0, 1.0, 1.0, 1.0]], dtype=torch.float64)
+    done = torch.tensor([[False] * 5, [True, False, True, False, False]])
+    st.update_block(rew, None, done)
+    assert st.acc.tolist() == [2.0 + 4.0, 4.0 + 16.0, 2.0, 20.0]
+    assert st.ret.tolist() == [0.0, 3.0, 0.0, 5.0, 6.0]
+    st.reset_acc()
+    assert st.acc.tolist() == [0.0] * 4 and st.ret.tolist() == [0.0, 3.0, 0.0, 5.0, 6.0]
