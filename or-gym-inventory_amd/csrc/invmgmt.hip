@@ -593,6 +593,10 @@ __device__ __forceinline__ void wg_lds_sync() {
 //                     action row, and the state / output stores
 // Both waves then store half of the observation tile.  Same arithmetic, in
 // the same order, as im_step_regs (inventory_management.py:224-352).
+// With the lookahead (AHEAD) the dynamics wave loads d from the cache itself,
+// so it computes as soon as its own loads land, and the waves meet only once,
+// when the tile is complete (the window wave leaves the newest row's words to
+// the dynamics wave).
 //
 // Demand lookahead (P.ahead: two slots of [state hi, state lo, demand, 32-bit
 // buffer] x Npad, alternating per launch).  The demand is a function of the
@@ -641,6 +645,13 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
 #endif
         return x < 0 ? 0 : x;
     };
+    // DEC: with the lookahead the dynamics wave loads d itself and the waves
+    // meet once (tile complete); otherwise d is handed over at a first barrier
+#ifdef INVSIM_IM_SPLIT_DSYNC   // A/B build only: the round-5 handoff of d through LDS
+    constexpr bool DEC = false;
+#else
+    constexpr bool DEC = AHEAD;
+#endif
     const int bid = (int)blockIdx.x;
     TPROBE(0);
     TPROBE_ID();
@@ -708,6 +719,8 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
     // the tile halves each wave stores (16-byte aligned: an even int64 count)
     const int64_t tcount = (int64_t)nvalid * O;
     const int64_t thalf = ((tcount / 2) + 1) & ~(int64_t)1;
+    constexpr int WL = im_wlane(M1);
+    const bool wreg = (D - 1) * M1 <= WL;   // launch-uniform
     if (demand_wave) {
         const int64_t ee = valid ? e : N - 1;        // padded lanes: the last env's stream
         TableStage ts;
@@ -715,7 +728,7 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         uint64_t u32 = 0;
         int64_t d = 0;
         if (AHEAD) {
-            d = (int64_t)Acur[2 * S + ee];
+            if (!DEC) d = (int64_t)Acur[2 * S + ee];   // (DEC: the dynamics wave loads it)
         } else {
             ts = stage_table(lane);
             P.cm.rng.load(ee, g);
@@ -730,8 +743,6 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
             slot = slot >= D ? slot - D : slot;
             return ((int64_t)slot * S + e) * M1;
         };
-        constexpr int WL = im_wlane(M1);
-        const bool wreg = (D - 1) * M1 <= WL;   // launch-uniform
         uint32_t wv[WL];
         {
             const int rmax = nw > 0 ? nw / M1 - 1 : 0;
@@ -751,13 +762,15 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
             ts.flush(lane);
             d = draw(g, u32);
         }
-        dsh[lane] = d;
+        if (!DEC) dsh[lane] = d;
         if (D > 0) {   // the window part of the obs rows; the newest row is the dynamics wave's
             if (wreg) {
                 bool wide = false;
 #pragma unroll
                 for (int u = 0; u < WL; u++) {
-                    if (u < (D - 1) * M1) w[u] = (u < nw) ? (int64_t)wv[u] : 0;
+                    // (not the newest row, nw .. nw + M1 - 1: the dynamics wave
+                    // writes it, with no barrier in between under DEC)
+                    if (u < (D - 1) * M1 && !(u >= nw && u < nw + M1)) w[u] = (u < nw) ? (int64_t)wv[u] : 0;
                     wide |= (u < nw) && wv[u] == IM_WIDE;
                 }
                 if (wide) {
@@ -772,8 +785,9 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
                 for (int q = n * M1; q < D * M1; q++) w[q] = 0;
             }
         }
-        wg_lds_sync();   // d and the window rows -> dynamics wave
-        TPROBE(6);       // the window wave past its first barrier
+        if (!DEC) wg_lds_sync();   // d -> dynamics wave
+        if (DEC) TWAIT();  // (TIMING build: probe 6 after the window rows land)
+        TPROBE(6);       // the window wave past its first barrier (DEC: window rows in)
         if constexpr (!RG::kCounter) {
             if (!AHEAD && valid) {   // committed generator state: after this step's draw
                 if (Acur) {          // into slot cur (the committed slot once the slots flip)
@@ -823,6 +837,9 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         ep_r = P.cm.ep_ret[valid ? e : N - 1];
     }
     int64_t req[M1], arr[M1], I[M1], B[M1 + 1];
+    // DEC: this step's demand straight from the lookahead slot, so the dynamics
+    // wave does not wait for the window wave's loads before its arithmetic
+    const int64_t d_ahead = DEC ? (int64_t)Acur[2 * S + (valid ? e : N - 1)] : 0;
 #pragma unroll
     for (int i = 0; i < M1; i++) req[i] = arow[i];
 #pragma unroll
@@ -855,9 +872,10 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
         Sv[i + 1] = R[i];                                           // :295
         U[i + 1] = wrap_sub(ordreq[i], R[i]);                       // :304
     }
-    wg_lds_sync();   // d from the demand wave
+    if (!DEC) wg_lds_sync();   // d from the demand wave
+    if (DEC) TWAIT();     // (TIMING build: probe 1 after the loads land)
     TPROBE_AT(1, WAVE);   // the dynamics wave: loads in, d handed over
-    const int64_t d = dsh[lane];
+    const int64_t d = DEC ? d_ahead : dsh[lane];
     const int64_t dfill = wrap_add(d, B[0]);                        // :284-286
     const int64_t s0 = Icur[0] < dfill ? Icur[0] : dfill;           // :288
     Icur[0] = wrap_sub(Icur[0], s0);

@@ -7,7 +7,7 @@ waves (profiling only; needs the TIMING build, csrc `make timing`).
 Probes (s_memrealtime, 100 MHz): 0 workgroup entry (thread 0); lookahead
 1 loads + RHS table in LDS, 2 demand drawn, 5 exit; step 3 / 4 dynamics wave
 entry / exit, 1 its loads in and d handed over, 2 its step computed (tile
-complete), 6 / 5 window wave past its first barrier / exit.
+complete), 6 / 5 window wave: rows landed / exit.
 """
 import ctypes as C
 import os
@@ -53,9 +53,9 @@ def main():
     print(f"-- step: {nst} workgroups")
     print("  entry             " + fmt(st[:, 0] - t0))
     print("  window exit       " + fmt(st[:, 5] - t0))
-    print("  window barrier 1  " + fmt(st[:, 6] - t0))
+    print("  window rows in    " + fmt(st[:, 6] - t0))
     print("  dynamics entry    " + fmt(st[:, 3] - t0))
-    print("  dynamics d in     " + fmt(st[:, 1] - t0))
+    print("  dynamics loads in " + fmt(st[:, 1] - t0))
     print("  dynamics computed " + fmt(st[:, 2] - t0))
     print("  dynamics exit     " + fmt(st[:, 4] - t0))
     print("  (computed - d in) " + fmt(st[:, 2] - st[:, 1]))
