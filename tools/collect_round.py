@@ -39,6 +39,28 @@ def kernel_avg_ns(csv_path, kern):
     return None
 
 
+def median_trace(prof, wl, kern, dst):
+    """gpu_round.sh trace3: three kernel-trace runs of the step bench (trace,
+    trace_2, trace_3).  The run whose dominant-kernel mean is the median becomes
+    trace/run_kernel_stats.csv (run 1's file is kept beside it as
+    run_kernel_stats.run1.csv); the three means go to
+    profiles/<round>/<workload>_step_trace_runs.json."""
+    runs = [d for d in ("trace", "trace_2", "trace_3") if os.path.exists(os.path.join(prof, d, "run_kernel_stats.csv"))]
+    if len(runs) < 3:
+        return
+    keep = os.path.join(prof, "trace", "run_kernel_stats.run1.csv")
+    if not os.path.exists(keep):
+        shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"), keep)
+    paths = {d: keep if d == "trace" else os.path.join(prof, d, "run_kernel_stats.csv") for d in runs}
+    ns = {d: kernel_avg_ns(p, kern) for d, p in paths.items()}
+    order = sorted(runs, key=lambda d: ns[d])
+    med = order[1]
+    shutil.copy(paths[med], os.path.join(prof, "trace", "run_kernel_stats.csv"))
+    with open(os.path.join(dst, f"{wl}_step_trace_runs.json"), "w") as f:
+        json.dump({"kernel": kern, "mean_ns_per_run": ns, "kept": med,
+                   "rule": "median of three rocprofv3 --kernel-trace --stats runs of the step bench"}, f, indent=1)
+
+
 def issue_frac(src, wl, mode, kern_ms):
     """Newsvendor's issue-rate roofline from this round's SQ passes (bench.py
     _issue): VALU + SALU wave-instructions per launch over 1 024 SIMDs x the
@@ -67,6 +89,7 @@ def main():
     for wl, kern in KERNELS.items():
         prof = os.path.join(src, f"prof_{wl}")
         if os.path.isdir(prof):
+            median_trace(prof, wl, kern, dst)
             shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"),
                         os.path.join(dst, f"{wl}_step_kernel_stats.csv"))
             roll = os.path.join(prof, "trace_roll", "run_kernel_stats.csv")

@@ -5,10 +5,10 @@
 # Newsvendor step and rollout kernels.  Everything lands in
 # gpurun_out/round_TAG/.  Stops at the first failing step (no GPU work after a
 # fault/timeout).
-#   tools/gpu_round.sh TAG [tests|bench|prof|sq ...]   (default: all)
+#   tools/gpu_round.sh TAG [tests|bench|prof|trace3|sq ...]   (default: all)
 set -u
 TAG=${1:-r01}; shift || true
-PARTS=${*:-tests bench prof sq}
+PARTS=${*:-tests bench prof trace3 sq}
 OUT=gpurun_out/round_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -59,6 +59,18 @@ for part in $PARTS; do
           python bench.py --workload $w --mode policy --steps 600 --warmup 60 $B > $P.fetch_pol.log 2>&1
       run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/pmc_write_pol -o run -- \
           python bench.py --workload $w --mode policy --steps 600 --warmup 60 $B > $P.write_pol.log 2>&1
+    done ;;
+  trace3)
+    # two more kernel-trace runs of each step bench (trace_2, trace_3): a
+    # dispatch's rocprofv3 mean moves by up to ~8 % between processes on one
+    # box (profiles/r06/split_dec/rocprof_ab.md), so collect_round.py keeps the
+    # median of the three runs
+    for w in $WLS; do
+      P=$OUT/prof_$w
+      for r in 2 3; do
+        run timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace_$r -o run -- \
+            python bench.py --workload $w --steps 1000 --warmup 50 $B > $P.trace_$r.log 2>&1
+      done
     done ;;
   sq)
     # Newsvendor step (nv_step1_kernel) and rollout (nv_roll_kernel): issue vs wait
