@@ -224,6 +224,7 @@ Knobs read_knobs() {
         }
     };
     count("INVSIM_IM_ROLL3O_MAX_N", k.im_roll3o_max_n);
+    count("INVSIM_IM_ROLL_SUB", k.im_roll_sub);
     count("INVSIM_NET_ROLLQ_MAX_N", k.net_rollq_max_n);
     count("INVSIM_NET_ROLL4_MAX_N", k.net_roll4_max_n);
     k.nv_xcd = env_flag("INVSIM_NV_XCD", k.nv_xcd);

@@ -1072,7 +1072,7 @@ struct ImLt3 {
 // take AGPRs beyond them: one wave per SIMD, measured 104 -> 166 us)
 template <int L0, int L1, int L2, bool BACKLOG, bool POL, class RG = Pcg>
 __global__ void __launch_bounds__(2 * WAVE) __attribute__((amdgpu_waves_per_eu(2)))
-im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO pol) {
+im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO pol, int g0) {
     using G = ImLt3<L0, L1, L2>;
     constexpr int M1 = G::M1, D = G::D, O = G::O, CH = G::CH;
     extern __shared__ __attribute__((aligned(16))) int64_t im_tile[];
@@ -1081,7 +1081,7 @@ im_roll3_kernel(ImParams P, int t_start, StepIO<int64_t, int64_t> io, PolicyIO p
     const int lane = threadIdx.x & (WAVE - 1);
     const int64_t N = P.cm.N;
     const int64_t S = P.cm.Npad;
-    const int64_t e0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t e0 = ((int64_t)blockIdx.x + g0) * WAVE;   // g0: the launch's first group
     const int64_t e = e0 + lane;
     const bool valid = e < N;
     const int64_t el = valid ? e : N - 1;          // padded lanes: the last env's data, never stored
@@ -1856,11 +1856,21 @@ hipError_t im_roll_launch(const ImParams &p, bool backlog, int t_u, const Policy
     const bool g2 = p.cm.kn.im_roll3o_g2 < 0 ? pol != nullptr : p.cm.kn.im_roll3o_g2 == 1;
     const bool two = three && g2 && (g3.x % 2) == 0;
     const dim3 g6(g3.x / 2);
+    // INVSIM_IM_ROLL_SUB (default 65 536): the 2-role rollout as back-to-back
+    // launches of at most that many envs (whole 64-env groups), each over its
+    // own groups: one round of 1 024 workgroups (four per CU) per launch.
+    // Measured at K = 30 (profiles/r06/roll_sub): 262 144 envs 618 -> 564 us,
+    // 1 048 576 envs 2 433 -> 2 300 us; sub-launches of 131 072 envs (two
+    // rounds each) are slower than one launch, of 16 384 far slower
+    const int sub = p.cm.kn.im_roll_sub >= WAVE ? (int)(p.cm.kn.im_roll_sub / WAVE) : (int)g3.x;
 #define R_(B, POL)                                                                                                    \
     do {                                                                                                              \
         if (two) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, B, POL, RG, 2>), g6, dim3(6 * WAVE), 2 * G3::lds(POL), s, p, t_u, io, pv); \
         else if (three) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, B, POL, RG>), g3, dim3(3 * WAVE), G3::lds(POL), s, p, t_u, io, pv); \
-        else hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, B, POL, RG>), g3, dim3(2 * WAVE), G::lds(), s, p, t_u, io, pv);            \
+        else                                                                                                          \
+            for (int g0 = 0; g0 < (int)g3.x; g0 += sub)                                                               \
+                hipLaunchKernelGGL((im_roll3_kernel<1, 5, 10, B, POL, RG>), dim3(min(sub, (int)g3.x - g0)), dim3(2 * WAVE), \
+                                   G::lds(), s, p, t_u, io, pv, g0);                                                  \
     } while (0)
     if (pol) {
         if (backlog) R_(true, true);

@@ -115,6 +115,7 @@ struct Knobs {
     bool net_ahead = true;           // INVSIM_NET_AHEAD=0: no demand lookahead
     bool net_generic = false;        // INVSIM_NET_GENERIC=1: the generic kernel for the built-in graphs
     int64_t im_roll3o_max_n = 32768; // INVSIM_IM_ROLL3O_MAX_N: largest batch for the 3-role rollout
+    int64_t im_roll_sub = 65536;     // INVSIM_IM_ROLL_SUB: 2-role rollouts as back-to-back launches of at most this many envs (0: one launch)
     int64_t net_roll4_max_n = 16384; // INVSIM_NET_ROLL4_MAX_N: largest batch for the 4-role Net rollout (0: never)
     int64_t net_rollq_max_n = 0;     // INVSIM_NET_ROLLQ_MAX_N: largest batch for the 16-lane-row Net rollout
                                      //   (net_rollq_kernel; 0 = never, the default: measured 6 % slower than
