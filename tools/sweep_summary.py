@@ -28,6 +28,9 @@ sys.path.insert(0, ROOT)
 from bench import HBM_PEAK_GBS, WORKLOADS  # noqa: E402
 
 
+ROLL_SUB = 65536   # envs per im_roll3_kernel launch (csrc kernels.hpp im_roll_sub)
+
+
 def last_json(path):
     for line in reversed(open(path).read().strip().split("\n")):
         line = line.strip()
@@ -69,7 +72,10 @@ def sweep(meas, out):
             fetch = counter(os.path.join(d, "pmc_fetch" + sfx), "FETCH_SIZE", kname)
             write = counter(os.path.join(d, "pmc_write" + sfx), "WRITE_SIZE", kname)
             B = wl["B_io"] + (wl["B_state"] if K == 1 else wl["B_state_rollout"] / K)
-            alg = B * n * K
+            # per dispatch: since round 6 a rollout past 65 536 envs is back-to-back
+            # launches of 65 536 envs (INVSIM_IM_ROLL_SUB's default), and rocprofv3 /
+            # the counters report per launch
+            alg = B * (n if K == 1 else min(n, ROLL_SUB)) * K
             ns = float(k["AverageNs"]) if k else None
             hbm = 2.0 * fetch * 1024 + write * 1024 if fetch is not None and write is not None else None
             res.append({
