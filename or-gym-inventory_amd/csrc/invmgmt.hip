@@ -1862,7 +1862,7 @@ hipError_t im_roll_launch(const ImParams &p, bool backlog, int t_u, const Policy
     // Measured at K = 30 (profiles/r06/roll_sub): 262 144 envs 618 -> 564 us,
     // 1 048 576 envs 2 433 -> 2 300 us; sub-launches of 131 072 envs (two
     // rounds each) are slower than one launch, of 16 384 far slower
-    const int sub = p.cm.kn.im_roll_sub >= WAVE ? (int)(p.cm.kn.im_roll_sub / WAVE) : (int)g3.x;
+    const int sub = p.cm.kn.im_roll_sub >= WAVE ? (int)std::min<int64_t>(p.cm.kn.im_roll_sub / WAVE, g3.x) : (int)g3.x;
 #define R_(B, POL)                                                                                                    \
     do {                                                                                                              \
         if (two) hipLaunchKernelGGL((im_roll3o_kernel<1, 5, 10, B, POL, RG, 2>), g6, dim3(6 * WAVE), 2 * G3::lds(POL), s, p, t_u, io, pv); \
