@@ -721,6 +721,28 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
     const int64_t thalf = ((tcount / 2) + 1) & ~(int64_t)1;
     constexpr int WL = im_wlane(M1);
     const bool wreg = (D - 1) * M1 <= WL;   // launch-uniform
+    // window rows t+1-n .. t-1 (:380), loaded whole (see im_step_regs)
+    const int slot0 = D > 0 ? (int)((uint32_t)(t1 - n) % (uint32_t)D) : 0;
+    auto wrow = [&](int r) -> int64_t {
+        int slot = slot0 + r;
+        slot = slot >= D ? slot - D : slot;
+        return ((int64_t)slot * S + e) * M1;
+    };
+    // DEC with a register window: the dynamics wave, whose own loads land
+    // ~1.4 us before the window wave's (profiles/r06/split_dec), loads the
+    // window rows RW .. RWN-1 and writes their tile words; the window wave the
+    // rest.  RW = 6 of 9 measured fastest (Backlog 65 536 8.13 -> 7.81 us,
+    // LostSales 32 768 6.19 -> 5.99 us; RW = 4, 5, 7 in between).  rmax: the last row that holds a logged order (earlier periods
+    // re-read it: straight-line loads, entries past nw unused)
+#ifndef INVSIM_IM_SPLIT_RW
+#define INVSIM_IM_SPLIT_RW 6
+#endif
+    constexpr int RWN = WL / M1;
+    constexpr int RW = INVSIM_IM_SPLIT_RW < RWN ? INVSIM_IM_SPLIT_RW : RWN;
+    constexpr int WD = (RWN - RW) * M1 > 0 ? (RWN - RW) * M1 : 1;
+    const bool wsplit = DEC && wreg && RW < RWN;
+    const int u_dyn = wsplit ? RW * M1 : WL;   // log entries u_dyn <= u < nw: the dynamics wave's
+    const int rmax = nw > 0 ? nw / M1 - 1 : 0;
     if (demand_wave) {
         const int64_t ee = valid ? e : N - 1;        // padded lanes: the last env's stream
         TableStage ts;
@@ -736,25 +758,22 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
             g.sub(0);
             if (NPD && !RG::kCounter) u32 = P.cm.u32buf[ee];
         }
-        // window rows t+1-n .. t-1 (:380), loaded whole (see im_step_regs)
-        const int slot0 = D > 0 ? (int)((uint32_t)(t1 - n) % (uint32_t)D) : 0;
-        auto wrow = [&](int r) -> int64_t {
-            int slot = slot0 + r;
-            slot = slot >= D ? slot - D : slot;
-            return ((int64_t)slot * S + e) * M1;
-        };
         uint32_t wv[WL];
         {
-            const int rmax = nw > 0 ? nw / M1 - 1 : 0;
 #pragma unroll
-            for (int r = 0; r < WL / M1; r++) {
+            for (int r = 0; r < RWN; r++) {
 #ifdef INVSIM_ABL_NO_WINDOW   // profiling ablation build only (wrong results): no window read
 #pragma unroll
                 for (int i = 0; i < M1; i++) wv[r * M1 + i] = (uint32_t)(r + i);
 #else
-                const uint32_t *src = P.alog32 + wrow(r < rmax ? r : rmax);
+                if (r < RW || !wsplit) {
+                    const uint32_t *src = P.alog32 + wrow(r < rmax ? r : rmax);
 #pragma unroll
-                for (int i = 0; i < M1; i++) wv[r * M1 + i] = src[i];
+                    for (int i = 0; i < M1; i++) wv[r * M1 + i] = src[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < M1; i++) wv[r * M1 + i] = 0;   // (the dynamics wave's rows)
+                }
 #endif
             }
         }
@@ -770,13 +789,15 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
                 for (int u = 0; u < WL; u++) {
                     // (not the newest row, nw .. nw + M1 - 1: the dynamics wave
                     // writes it, with no barrier in between under DEC)
-                    if (u < (D - 1) * M1 && !(u >= nw && u < nw + M1)) w[u] = (u < nw) ? (int64_t)wv[u] : 0;
-                    wide |= (u < nw) && wv[u] == IM_WIDE;
+                    // (nor the log entries u_dyn .. nw - 1: the dynamics wave's under wsplit)
+                    if (u < (D - 1) * M1 && !(u >= nw && u < nw + M1) && !(u >= u_dyn && u < nw))
+                        w[u] = (u < nw) ? (int64_t)wv[u] : 0;
+                    wide |= (u < nw) && (u < u_dyn) && wv[u] == IM_WIDE;
                 }
                 if (wide) {
 #pragma unroll
                     for (int u = 0; u < WL; u++)
-                        if (u < nw && wv[u] == IM_WIDE) w[u] = P.alog[wrow(u / M1) + u % M1];
+                        if (u < nw && u < u_dyn && wv[u] == IM_WIDE) w[u] = P.alog[wrow(u / M1) + u % M1];
                 }
                 if (n < D)
                     for (int q = (D - 1) * M1; q < D * M1; q++) w[q] = 0;
@@ -840,6 +861,20 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
     // DEC: this step's demand straight from the lookahead slot, so the dynamics
     // wave does not wait for the window wave's loads before its arithmetic
     const int64_t d_ahead = DEC ? (int64_t)Acur[2 * S + (valid ? e : N - 1)] : 0;
+    uint32_t wd[WD];   // wsplit: window rows RW .. RWN-1
+    if (wsplit) {
+#pragma unroll
+        for (int r = RW; r < RWN; r++) {
+#ifdef INVSIM_ABL_NO_WINDOW
+#pragma unroll
+            for (int i = 0; i < M1; i++) wd[(r - RW) * M1 + i] = (uint32_t)(r + i);
+#else
+            const uint32_t *src = P.alog32 + wrow(r < rmax ? r : rmax);
+#pragma unroll
+            for (int i = 0; i < M1; i++) wd[(r - RW) * M1 + i] = src[i];
+#endif
+        }
+    }
 #pragma unroll
     for (int i = 0; i < M1; i++) req[i] = arow[i];
 #pragma unroll
@@ -896,6 +931,13 @@ im_split_kernel(ImParams P, int t, StepIO<int64_t, int64_t> io, int cur, int la0
     if (D > 0) {
 #pragma unroll
         for (int i = 0; i < M1; i++) w[(n - 1) * M1 + i] = req[i];  // newest row last (:380)
+    }
+    if (wsplit) {   // its window rows (an entry >= 2^32 - 1 from the int64 side ring)
+#pragma unroll
+        for (int j = 0; j < (RWN - RW) * M1; j++) {
+            const int u = RW * M1 + j;
+            if (u < nw) w[u] = wd[j] == IM_WIDE ? P.alog[wrow(u / M1) + u % M1] : (int64_t)wd[j];
+        }
     }
     wg_lds_sync();   // tile complete
     TPROBE_AT(2, WAVE);   // the dynamics wave: step computed, stores next
